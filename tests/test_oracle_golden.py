@@ -1,0 +1,66 @@
+"""The oracle restatements against fixtures produced by the reference GLL.py itself.
+
+This pins the oracle before it is trusted as the checker of the HIP path (CPU only)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gll_oracle as O
+from oracle import gll_port as PT
+from tests.golden_io import Case, names
+
+CASES = names()
+
+
+def test_fixtures_present():
+    assert len(CASES) >= 10
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_inputs_regenerate_bit_exact(name):
+    assert Case(name).x_ok, "synthetic X differs from the fixture's sha256"
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_matches_reference(name):
+    c = Case(name)
+    ind, _ = O.knn_exact(c.X, c.k)
+    assert np.array_equal(ind, c.knn)
+    U, st = O.forward(c.X, c.Y, c.tau, c.eps, c.k)
+    assert O.rel_err(U, c.U) < 1e-12
+    grad = O.backward(st, c.gbar)
+    # the reference casts the edge values to fp32 before G @ X (GLL.py:154): fp32 floor
+    assert c.grad_error(grad, O.rel_err) < 2e-6
+
+
+@pytest.mark.parametrize("name", [n for n in CASES if n.startswith(("plumbing", "ns"))])
+def test_port_matches_reference(name):
+    c = Case(name)
+    Xt = torch.from_numpy(c.X).requires_grad_(True)
+    U, saved = PT.forward(Xt, torch.from_numpy(c.Y), c.tau, c.eps, c.k)
+    assert O.rel_err(U.numpy(), c.U) < 1e-12
+    g = PT.backward(saved, torch.from_numpy(c.gbar)).numpy()
+    assert c.grad_error(g, O.rel_err) < 2e-6
+
+
+def test_oracle_with_given_knn_equals_search():
+    c = Case(CASES[0])
+    U1, _ = O.forward(c.X, c.Y, c.tau, c.eps, c.k)
+    U2, _ = O.forward(c.X, c.Y, c.tau, c.eps, c.k, knn=(c.knn, None))
+    assert O.rel_err(U2, U1) < 1e-12
+
+
+def test_fd_gradient_plumbing():
+    """Backward is the exact gradient of forward for a frozen graph."""
+    c = Case("plumbing_epsauto_tau0p07_f32")
+    X = c.X.astype(np.float64)
+    U, st = O.forward(X, c.Y, c.tau, c.eps, c.k)
+    g = O.backward(st, c.gbar)
+    rng = np.random.default_rng(0)
+    D = rng.standard_normal(X.shape)
+    h = 1e-6
+    Up, _ = O.forward(X + h * D, c.Y, c.tau, c.eps, c.k, knn=(c.knn, None))
+    Um, _ = O.forward(X - h * D, c.Y, c.tau, c.eps, c.k, knn=(c.knn, None))
+    fd = np.sum((Up - Um) * c.gbar) / (2 * h)
+    an = np.sum(g * D)
+    assert abs(fd - an) / abs(an) < 1e-6
