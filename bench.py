@@ -1,0 +1,250 @@
+"""GLL fwd+bwd throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ns|fullysup|stress|plumbing]
+    torchrun --nproc-per-node N bench.py --gpus N ...        (one process per GPU)
+
+One step = one `LaplaceLearningSparseHard.apply` forward (kNN graph built from scratch)
++ the backward of a fixed seeded upstream gradient dL/dU, on the rank's own synthetic
+minibatch graph (seed = rank; SURVEY.md §8d generator), plus the asynchronous RCCL
+all_gather of the predictions U that the sharded path performs (§8e).  Inputs are resident
+in HBM before timing starts.  Rank 0 prints ONE JSON line; `value` = calls/s over all ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from graphlearninglayer_amd import GLL, _lib  # noqa: E402
+from graphlearninglayer_amd.parallel import gather_predictions, shard_rank_seed  # noqa: E402
+from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth  # noqa: E402
+
+METRIC = "GLL fwd+bwd calls/sec (base=500,batch=500,d=512,k=10) at 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+MFMA_F32_PEAK_TFS = 157.3    # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), spec
+EPS = {"plumbing": 1.0, "ns": 1.0, "fullysup": 1.0, "stress": "auto"}
+TAU = {"plumbing": 0.07, "ns": 0.07, "fullysup": 0.07, "stress": 0.07}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="ns", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="budget of the CPU-baseline sample (rank 0, N=1 only); 0 disables")
+    ap.add_argument("--no-profile", action="store_true", help="skip kernel event timing")
+    return ap.parse_args()
+
+
+def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps):
+    """Algorithmic work per launch of each kernel (SURVEY.md §8d byte/flop model)."""
+    n, d, K, m, C = cfg["n"], cfg["d"], cfg["k"], cfg["batch"], 10
+    E, nnz_uu = graph_stats
+    b_spmv = 8 * nnz_uu + 8 * m + 8 * m * C
+    cg_iter = b_spmv + 28 * m * C
+    u = {
+        "gram_d2_kernel": ("mfma", 2.0 * n * n * d),
+        "knn_select_kernel": ("hbm", 4.0 * n * n + 8.0 * n * K),
+        "pair_flag_kernel": ("hbm", 8.0 * n * K + n * K),
+        "row_scan_kernel": ("hbm", 12.0 * n),
+        "fill_kernel": ("hbm", 8.0 * n * K + n * K + 8.0 * E),
+        "row_finalize_kernel": ("hbm", 8.0 * E + 4 * n + 4 * m * C + 12.0 * E),
+        "cg_luu_kernel": ("hbm", 0.5 * (iters_fwd + iters_bwd) * cg_iter),
+        "edge_coef_kernel": ("hbm", 16.0 * E + 8.0 * n * C),
+        "grad_spmm_kernel": ("hbm", (12.0 * E + 8.0 * n * d) if auto_eps
+                             else (8.0 * E + 8.0 * n * C + 8.0 * n * d)),
+    }
+    return u
+
+
+def cpu_baseline(cfg, eps, tau, seconds):
+    """Time the reference's CPU step sequence (oracle/gll_port.py, 'port') on this host."""
+    from oracle import gll_port
+
+    X, lab = synth(cfg["base"], cfg["batch"], cfg["d"], r=cfg["r"], seed=0)
+    Y = torch.from_numpy(one_hot(lab[: cfg["base"]]))
+    g = torch.from_numpy(seeded_gbar(cfg["batch"], 10))
+    Xt = torch.from_numpy(X)
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or len(times) < 3:
+        t0 = time.perf_counter()
+        U, saved = gll_port.forward(Xt, Y, tau, eps, cfg["k"])
+        gll_port.backward(saved, g)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": round(1.0 / med, 3), "unit": "calls/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{len(times)} fwd+bwd calls of oracle/gll_port.py (reference step "
+                      f"sequence: exact kNN + scipy CSR + SuperLU + torch sparse mm) on "
+                      f"{cfg['base']}+{cfg['batch']}x{cfg['d']} k={cfg['k']}, median",
+            "host": platform.processor() or platform.machine(), "nproc": os.cpu_count()}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    c = dict(CONFIGS[a.config])
+    c["n"] = c["base"] + c["batch"]
+    eps, tau, k = EPS[a.config], TAU[a.config], c["k"]
+    X_np, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=shard_rank_seed(0, rank))
+    X = torch.from_numpy(X_np).to(dev).requires_grad_(True)
+    Y = torch.from_numpy(one_hot(lab[: c["base"]])).to(dev)
+    gbar = torch.from_numpy(seeded_gbar(c["batch"], 10, 1234 + rank)).to(dev)
+    lap = GLL.LaplaceLearningSparseHard.apply
+    GLL.CHECK_STATUS = True
+
+    def step():
+        U = lap(X, Y, tau, eps, k)
+        _, work = gather_predictions(U, async_op=True)
+        (gx,) = torch.autograd.grad(U, X, gbar)
+        if work is not None:
+            work.wait()
+        return U, gx
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # which kernel dominates: one untimed instrumented pass over all kernels
+    names = [_lib.kernel_name(q) for q in range(_lib.K_COUNT)]
+    per_kernel = {}
+    dominant = None
+    if not a.no_profile:
+        for q in range(_lib.K_COUNT):
+            _lib.prof_enable(q, True)
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize()
+        for q in range(_lib.K_COUNT):
+            ms, cnt = _lib.prof_read(q)
+            _lib.prof_enable(q, False)
+            if cnt:
+                per_kernel[names[q]] = {"us_per_launch": round(1e3 * ms / cnt, 3),
+                                        "launches_per_step": cnt / 10}
+        dominant = max(per_kernel, key=lambda kn: per_kernel[kn]["us_per_launch"]
+                       * per_kernel[kn]["launches_per_step"])
+        _lib.prof_enable(names.index(dominant), True)
+
+    # timed region
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        U, gx = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    roofline = None
+    if dominant is not None:
+        ms, cnt = _lib.prof_read(names.index(dominant))
+        _lib.prof_enable(names.index(dominant), False)
+        g = GLL.device_graph(X.detach(), k, eps)
+        rp = g["row_ptr"].cpu().numpy()
+        col = g["col"].cpu().numpy()
+        rows = np.repeat(np.arange(c["n"]), np.diff(rp))
+        nnz_uu = int(np.sum((rows >= c["base"]) & (col >= c["base"])))
+        GLL._poll_status(block=True)
+        iters = _cg_iters(X, Y, tau, eps, k, gbar)
+        units = kernel_units(c, (int(rp[-1]), nnz_uu), iters[0], iters[1], isinstance(eps, str))
+        bound, work = units[dominant]
+        avg_s = ms / cnt / 1e3
+        if bound == "mfma":
+            achieved, peak, unit = work / avg_s / 1e12, MFMA_F32_PEAK_TFS, "TFLOP/s"
+        else:
+            achieved, peak, unit = work / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
+        roofline = {"kernel": dominant, "bound": bound, "achieved": round(achieved, 3),
+                    "peak": peak, "unit": unit, "frac": round(achieved / peak, 5),
+                    "traffic": None, "work_per_launch": work,
+                    "avg_launch_us": round(avg_s * 1e6, 3), "launches": cnt,
+                    "cg_iters_fwd_bwd": list(iters)}
+        for kn, v in per_kernel.items():
+            b_, w_ = units[kn]
+            v["algorithmic"] = (f"{w_ / 1e9:.4g} GFLOP" if b_ == "mfma" else f"{w_ / 1e6:.4g} MB")
+
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_seconds > 0:
+        cpu = cpu_baseline(c, eps, tau, a.cpu_seconds)
+
+    if rank == 0:
+        calls = world * a.steps
+        out = {
+            "metric": METRIC,
+            "value": round(calls / elapsed, 3),
+            "unit": "calls/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1e3 * elapsed / a.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (latent-mixture unit-norm features, SURVEY.md §8d; seed = rank)",
+            "config": {"workload": a.config, "base": c["base"], "batch": c["batch"], "d": c["d"],
+                       "k": k, "eps": eps, "tau": tau, "classes": 10,
+                       "parallelism": f"dp{world}", "upstream_grad": "fixed seeded dL/dU",
+                       "collective": "all_gather(U) per step" if world > 1 else "none"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernels": per_kernel,
+        }
+        if cpu:
+            out["speedup_vs_cpu"] = round(out["value"] / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _cg_iters(X, Y, tau, eps, k, gbar):
+    """CG iterations (max over columns) of one fwd and one bwd solve on the bench input."""
+    import ctypes as ct
+
+    n, d = X.shape
+    base, C = Y.shape
+    prob = GLL.make_problem(n, d, base, C, k, tau, eps)
+    lib = _lib.lib()
+    ws = torch.empty(lib.gll_workspace_bytes(ct.byref(prob)), dtype=torch.uint8, device=X.device)
+    U = torch.empty(n - base, C, dtype=torch.float64, device=X.device)
+    X32 = X.detach().contiguous()
+    Yc = Y.contiguous()
+    s = torch.cuda.current_stream(X.device).cuda_stream
+    _lib.check(lib.gll_forward(ct.byref(prob), X32.data_ptr(), Yc.data_ptr(), _lib.GLL_DT_F32,
+                               ws.data_ptr(), U.data_ptr(), s), "gll_forward")
+    gx = torch.empty(n, d, dtype=torch.float32, device=X.device)
+    _lib.check(lib.gll_backward(ct.byref(prob), X32.data_ptr(), None, 0, ws.data_ptr(),
+                                gbar.data_ptr(), _lib.GLL_DT_F64, gx.data_ptr(), s),
+               "gll_backward")
+    st = ws[: 4 * _lib.ST_NWORDS].view(torch.int32).cpu().tolist()
+    return st[_lib.ST_FWD_ITERS], st[_lib.ST_BWD_ITERS]
+
+
+if __name__ == "__main__":
+    main()

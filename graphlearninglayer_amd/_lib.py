@@ -1,0 +1,105 @@
+"""ctypes binding of libgll.so (the C ABI of include/gll.h).
+
+The shared library is built in-tree by `graphlearninglayer_amd.build` (or
+`__graft_entry__.build()`).  There is no fallback: if it is missing, `lib()` raises.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgll.so")
+
+GLL_OK = 0
+GLL_DT_F32, GLL_DT_F64, GLL_DT_I64 = 0, 1, 2
+ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
+ST_NWORDS = 16
+K_GRAM, K_SELECT, K_MUTUAL, K_SCAN, K_FILL, K_FINALIZE, K_CG, K_EDGE, K_GRAD = range(9)
+K_COUNT = 9
+
+# every symbol include/gll.h declares (tests check the library exports all of them)
+EXPORTS = (
+    "gll_workspace_bytes", "gll_forward", "gll_backward", "gll_graph", "gll_workspace_view",
+    "gll_cg_csr_workspace_bytes", "gll_cg_csr", "gll_prof_enable", "gll_prof_read",
+    "gll_kernel_name", "gll_strerror",
+)
+
+
+class Problem(ct.Structure):
+    _fields_ = [
+        ("n", ct.c_int32), ("d", ct.c_int32), ("base", ct.c_int32), ("C", ct.c_int32),
+        ("K", ct.c_int32), ("max_iter", ct.c_int32), ("tau", ct.c_float), ("eps", ct.c_float),
+        ("rtol", ct.c_float), ("flags", ct.c_int32),
+    ]
+
+
+class View(ct.Structure):
+    _fields_ = [(name, ct.c_void_p) for name in (
+        "knn_idx", "knn_d2", "eps", "row_ptr", "col", "w", "d2", "deg", "U32", "wadj", "status")]
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _declare(lib):
+    P = ct.POINTER(Problem)
+    vp, i32, sz = ct.c_void_p, ct.c_int, ct.c_size_t
+    lib.gll_workspace_bytes.argtypes = [P]
+    lib.gll_workspace_bytes.restype = sz
+    lib.gll_forward.argtypes = [P, vp, vp, i32, vp, vp, vp]
+    lib.gll_forward.restype = i32
+    lib.gll_backward.argtypes = [P, vp, vp, i32, vp, vp, i32, vp, vp]
+    lib.gll_backward.restype = i32
+    lib.gll_graph.argtypes = [P, vp, vp, vp]
+    lib.gll_graph.restype = i32
+    lib.gll_workspace_view.argtypes = [P, vp, ct.POINTER(View)]
+    lib.gll_workspace_view.restype = i32
+    lib.gll_cg_csr_workspace_bytes.argtypes = [i32, i32]
+    lib.gll_cg_csr_workspace_bytes.restype = sz
+    lib.gll_cg_csr.argtypes = [i32, i32, vp, vp, vp, vp, vp, ct.c_float, i32, vp, vp, vp, vp]
+    lib.gll_cg_csr.restype = i32
+    lib.gll_prof_enable.argtypes = [i32, i32]
+    lib.gll_prof_enable.restype = i32
+    lib.gll_prof_read.argtypes = [i32, ct.POINTER(ct.c_double), ct.POINTER(ct.c_int)]
+    lib.gll_prof_read.restype = i32
+    lib.gll_kernel_name.argtypes = [i32]
+    lib.gll_kernel_name.restype = ct.c_char_p
+    lib.gll_strerror.argtypes = [i32]
+    lib.gll_strerror.restype = ct.c_char_p
+    return lib
+
+
+def lib():
+    """The loaded libgll.so.  Raises if the HIP library was not built."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise RuntimeError(
+                        f"{LIB_PATH} is missing: build the HIP extension first "
+                        "(python -m graphlearninglayer_amd.build). There is no CPU fallback.")
+                _lib = _declare(ct.CDLL(LIB_PATH))
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != GLL_OK:
+        raise RuntimeError(f"{what} failed: {lib().gll_strerror(rc).decode()} (code {rc})")
+
+
+def kernel_name(kid: int) -> str:
+    return lib().gll_kernel_name(kid).decode()
+
+
+def prof_enable(kid: int, on: bool = True):
+    check(lib().gll_prof_enable(kid, 1 if on else 0), "gll_prof_enable")
+
+
+def prof_read(kid: int):
+    ms, cnt = ct.c_double(0.0), ct.c_int(0)
+    check(lib().gll_prof_read(kid, ct.byref(ms), ct.byref(cnt)), "gll_prof_read")
+    return ms.value, cnt.value

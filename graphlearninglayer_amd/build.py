@@ -1,0 +1,89 @@
+"""Build libgll.so (HIP kernels + C ABI) for gfx950 with hipcc, in-tree.
+
+    python -m graphlearninglayer_amd.build [--force] [--verbose]
+
+The shared library lands next to this file so it travels to the GPU box with the repo
+snapshot (it is git-ignored).  Each translation unit is compiled separately (in parallel)
+and then linked; a unit is rebuilt only when it or a header is newer than its object.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+OBJ = os.path.join(HERE, "_obj")
+LIB = os.path.join(HERE, "libgll.so")
+ARCH = os.environ.get("GLL_OFFLOAD_ARCH", "gfx950")
+UNITS = ["knn.hip", "graph.hip", "cg.hip", "grad.hip", "api.hip"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
+         "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
+
+
+def hipcc():
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm >= 7 required)")
+
+
+def _headers_mtime():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hs.append(os.path.join(INCLUDE, "gll.h"))
+    return max(os.path.getmtime(h) for h in hs)
+
+
+def _compile(unit, force, verbose, extra):
+    src = os.path.join(CSRC, unit)
+    obj = os.path.join(OBJ, unit.replace(".hip", ".o"))
+    if (not force and os.path.exists(obj)
+            and os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime())):
+        return obj
+    cmd = [hipcc(), *FLAGS, *extra, "-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed on {unit}:\n{r.stdout}\n{r.stderr}")
+    if verbose and r.stderr.strip():
+        print(r.stderr, file=sys.stderr)
+    return obj
+
+
+def build(force=False, verbose=False, extra=()):
+    os.makedirs(OBJ, exist_ok=True)
+    jobs = min(len(UNITS), max(1, min(8, os.cpu_count() or 1)))
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda u: _compile(u, force, verbose, list(extra)), UNITS))
+    if (force or not os.path.exists(LIB)
+            or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs)):
+        cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    return LIB
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--resource-usage", action="store_true",
+                    help="print per-kernel VGPR/SGPR/LDS/occupancy (-Rpass-analysis)")
+    a = ap.parse_args()
+    extra = ["-Rpass-analysis=kernel-resource-usage"] if a.resource_usage else []
+    print(build(force=a.force or a.resource_usage, verbose=a.verbose or a.resource_usage,
+                extra=extra))
+
+
+if __name__ == "__main__":
+    main()

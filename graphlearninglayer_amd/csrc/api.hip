@@ -1,0 +1,233 @@
+// api.hip -- the extern "C" boundary declared in include/gll.h.
+//
+// Orchestrates the kernels of knn.hip, graph.hip, cg.hip and grad.hip on the caller's
+// stream.  No allocation, no host synchronisation: the caller owns the workspace (the
+// Python mirror takes it from torch's caching allocator) and keeps it alive from
+// gll_forward to gll_backward, as the reference keeps its graph on ctx (GLL.py:69-70).
+#include <mutex>
+#include <vector>
+
+#include "gll_internal.h"
+
+namespace gll {
+
+// ---------------------------------------------------------------------------------------
+// Instrumentation: optional HIP event brackets around selected kernels (bench.py uses
+// them to time the dominant kernel inside its timed region).
+// ---------------------------------------------------------------------------------------
+struct ProfState {
+    bool on[GLL_K_COUNT] = {};
+    std::vector<hipEvent_t> pending[GLL_K_COUNT];  // start, stop, start, stop, ...
+    std::vector<hipEvent_t> pool;
+    std::mutex mu;
+    hipEvent_t get() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        return e;
+    }
+};
+static ProfState g_prof;
+
+void prof_begin(int kid, hipStream_t s) {
+    if (!g_prof.on[kid]) return;
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    hipEvent_t e = g_prof.get();
+    if (!e) return;
+    hipEventRecord(e, s);
+    g_prof.pending[kid].push_back(e);
+}
+
+void prof_end(int kid, hipStream_t s) {
+    if (!g_prof.on[kid]) return;
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    if (g_prof.pending[kid].size() % 2 == 0) return;  // begin was not recorded
+    hipEvent_t e = g_prof.get();
+    if (!e) {
+        g_prof.pool.push_back(g_prof.pending[kid].back());
+        g_prof.pending[kid].pop_back();
+        return;
+    }
+    hipEventRecord(e, s);
+    g_prof.pending[kid].push_back(e);
+}
+
+static const char* kKernelNames[GLL_K_COUNT] = {
+    "gram_d2_kernel",   "knn_select_kernel", "pair_flag_kernel",
+    "row_scan_kernel",  "fill_kernel",       "row_finalize_kernel",
+    "cg_luu_kernel",    "edge_coef_kernel",  "grad_spmm_kernel"};
+
+static bool vec_ok(const float* X, int d) {
+    return (d % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+}
+
+static int check(const gll_problem* p) {
+    if (!p) return GLL_ERR_INVALID_ARG;
+    if (p->n < 2 || p->d < 1 || p->C < 1 || p->K < 2) return GLL_ERR_INVALID_ARG;
+    if (p->base < 0 || p->base > p->n) return GLL_ERR_INVALID_ARG;
+    const int K = p->K < p->n ? p->K : p->n;
+    if (K - 1 > 64) return GLL_ERR_UNSUPPORTED;      // candidate lists hold <= 64
+    if (p->C > 256) return GLL_ERR_UNSUPPORTED;       // rhs accumulators per lane
+    if ((p->d + 255) / 256 > 16) return GLL_ERR_UNSUPPORTED;  // d <= 4096 in the SpMM
+    if (int64_t(p->n) * K > INT32_MAX / 2) return GLL_ERR_UNSUPPORTED;
+    return GLL_OK;
+}
+
+static int hip_status(hipError_t e) { return e == hipSuccess ? GLL_OK : GLL_ERR_HIP; }
+
+static int build_graph(const gll_problem* p, const Layout& L, const float* X, void* ws,
+                       hipStream_t s) {
+    const bool vec = vec_ok(X, p->d);
+    const bool auto_eps = !(p->eps > 0.f);
+    int32_t* st = L.at<int32_t>(ws, L.status);
+    hipError_t e = launch_gram(X, L.n, L.d, L.at<float>(ws, L.D2), L.ldD, st, vec, s);
+    if (e != hipSuccess) return GLL_ERR_HIP;
+    e = launch_select(L.at<float>(ws, L.D2), L.ldD, X, L.n, L.d, L.K, p->eps, auto_eps,
+                      L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2),
+                      L.at<float>(ws, L.eps), L.at<int32_t>(ws, L.fwd_cnt),
+                      L.at<int32_t>(ws, L.rev_cnt), L.at<int32_t>(ws, L.fill_cnt), st, vec, s);
+    if (e != hipSuccess) return GLL_ERR_HIP;
+    return hip_status(launch_graph_build(L, ws, s));
+}
+
+}  // namespace gll
+
+using namespace gll;
+
+extern "C" {
+
+size_t gll_workspace_bytes(const gll_problem* p) {
+    if (check(p) != GLL_OK) return 0;
+    return Layout(*p).total;
+}
+
+int gll_graph(const gll_problem* p, const float* X, void* ws, void* stream) {
+    int rc = check(p);
+    if (rc != GLL_OK) return rc;
+    if (!X || !ws) return GLL_ERR_INVALID_ARG;
+    if (p->base != 0) return GLL_ERR_INVALID_ARG;  // graph only: no labeled block
+    Layout L(*p);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    rc = build_graph(p, L, X, ws, s);
+    if (rc != GLL_OK) return rc;
+    // base = 0: every row is "unlabeled", rhs = 0 and no label read
+    return hip_status(launch_finalize(L, ws, nullptr, GLL_DT_F32, p->tau, s));
+}
+
+int gll_forward(const gll_problem* p, const float* X, const void* Y, int y_dtype, void* ws,
+                double* U, void* stream) {
+    int rc = check(p);
+    if (rc != GLL_OK) return rc;
+    if (!X || !ws || (p->base > 0 && !Y) || (p->n > p->base && !U)) return GLL_ERR_INVALID_ARG;
+    Layout L(*p);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    rc = build_graph(p, L, X, ws, s);
+    if (rc != GLL_OK) return rc;
+    if (launch_finalize(L, ws, Y, y_dtype, p->tau, s) != hipSuccess) return GLL_ERR_HIP;
+    const float rtol = p->rtol > 0.f ? p->rtol : 1e-6f;
+    const int max_iter = p->max_iter > 0 ? p->max_iter : 1000;
+    int32_t* st = L.at<int32_t>(ws, L.status);
+    float* U32 = L.at<float>(ws, L.P) + size_t(L.base) * L.C;
+    return hip_status(launch_cg_luu(L, ws, L.at<float>(ws, L.rhs), GLL_DT_F32, U, U32, rtol,
+                                    max_iter, st + GLL_ST_FWD_NONCONV, st + GLL_ST_FWD_ITERS, s));
+}
+
+int gll_backward(const gll_problem* p, const float* X, const void* Y, int y_dtype, void* ws,
+                 const void* gbar, int g_dtype, float* gradX, void* stream) {
+    (void)Y;
+    (void)y_dtype;
+    int rc = check(p);
+    if (rc != GLL_OK) return rc;
+    if (!X || !ws || !gradX || (p->n > p->base && !gbar)) return GLL_ERR_INVALID_ARG;
+    if (g_dtype != GLL_DT_F32 && g_dtype != GLL_DT_F64) return GLL_ERR_INVALID_ARG;
+    Layout L(*p);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const float rtol = p->rtol > 0.f ? p->rtol : 1e-6f;
+    const int max_iter = p->max_iter > 0 ? p->max_iter : 1000;
+    int32_t* st = L.at<int32_t>(ws, L.status);
+    float* wU = L.at<float>(ws, L.Wadj) + size_t(L.base) * L.C;
+    // adjoint solve: Luu is symmetric, so Luu^-T gbar = Luu^-1 gbar (GLL.py:93)
+    hipError_t e = launch_cg_luu(L, ws, gbar, g_dtype, nullptr, wU, rtol, max_iter,
+                                 st + GLL_ST_BWD_NONCONV, st + GLL_ST_BWD_ITERS, s);
+    if (e != hipSuccess) return GLL_ERR_HIP;
+    const bool auto_eps = !(p->eps > 0.f);
+    return hip_status(launch_backward_grad(L, ws, X, auto_eps, gradX, vec_ok(X, p->d), s));
+}
+
+int gll_workspace_view(const gll_problem* p, void* ws, gll_view* out) {
+    int rc = check(p);
+    if (rc != GLL_OK) return rc;
+    if (!ws || !out) return GLL_ERR_INVALID_ARG;
+    Layout L(*p);
+    out->knn_idx = L.at<int32_t>(ws, L.knn_idx);
+    out->knn_d2 = L.at<float>(ws, L.knn_d2);
+    out->eps = L.at<float>(ws, L.eps);
+    out->row_ptr = L.at<int32_t>(ws, L.row_ptr);
+    out->col = L.at<int32_t>(ws, L.col);
+    out->w = L.at<float>(ws, L.w);
+    out->d2 = L.at<float>(ws, L.d2e);
+    out->deg = L.at<float>(ws, L.deg);
+    out->U32 = L.at<float>(ws, L.P) + size_t(L.base) * L.C;
+    out->wadj = L.at<float>(ws, L.Wadj) + size_t(L.base) * L.C;
+    out->status = L.at<int32_t>(ws, L.status);
+    return GLL_OK;
+}
+
+int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const float* val,
+               const float* b, float* x, float atol, int max_iter, int32_t* iters,
+               int32_t* nonconv, void* workspace, void* stream) {
+    if (m < 1 || C < 1 || !row_ptr || !col || !val || !b || !x) return GLL_ERR_INVALID_ARG;
+    return hip_status(launch_cg_csr(m, C, row_ptr, col, val, b, x, atol,
+                                    max_iter > 0 ? max_iter : 100000, iters, nonconv,
+                                    static_cast<float*>(workspace),
+                                    static_cast<hipStream_t>(stream)));
+}
+
+size_t gll_cg_csr_workspace_bytes(int m, int C) { return size_t(5) * m * C * sizeof(float); }
+
+int gll_prof_enable(int kid, int on) {
+    if (kid < 0 || kid >= GLL_K_COUNT) return GLL_ERR_INVALID_ARG;
+    g_prof.on[kid] = on != 0;
+    return GLL_OK;
+}
+
+int gll_prof_read(int kid, double* ms_total, int* count) {
+    if (kid < 0 || kid >= GLL_K_COUNT || !ms_total || !count) return GLL_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    auto& v = g_prof.pending[kid];
+    double tot = 0.0;
+    int cnt = 0;
+    for (size_t q = 0; q + 1 < v.size(); q += 2) {
+        if (hipEventSynchronize(v[q + 1]) != hipSuccess) return GLL_ERR_HIP;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, v[q], v[q + 1]) != hipSuccess) return GLL_ERR_HIP;
+        tot += ms;
+        ++cnt;
+    }
+    for (auto e : v) g_prof.pool.push_back(e);
+    v.clear();
+    *ms_total = tot;
+    *count = cnt;
+    return GLL_OK;
+}
+
+const char* gll_kernel_name(int kid) {
+    if (kid < 0 || kid >= GLL_K_COUNT) return "?";
+    return kKernelNames[kid];
+}
+
+const char* gll_strerror(int code) {
+    switch (code) {
+        case GLL_OK: return "ok";
+        case GLL_ERR_INVALID_ARG: return "invalid argument";
+        case GLL_ERR_UNSUPPORTED: return "unsupported problem size (see include/gll.h limits)";
+        case GLL_ERR_HIP: return "HIP launch error";
+        default: return "unknown error";
+    }
+}
+
+}  // extern "C"

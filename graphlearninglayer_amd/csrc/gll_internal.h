@@ -1,0 +1,133 @@
+// gll_internal.h -- workspace layout, device helpers and launcher declarations shared by
+// the HIP translation units of libgll.  CDNA4 (gfx950) only: wave64, fp32 MFMA.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gll.h"
+
+namespace gll {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------------------------------
+// Workspace layout.  One block per forward/backward pair, carved into 256-B aligned arrays.
+// All sizes are functions of (n, d, base, C, K) only, so forward and backward agree.
+// ---------------------------------------------------------------------------------------
+struct Layout {
+    int n, d, base, m, C, K;
+    int ldD;          // leading dimension of the n x n squared-distance matrix
+    int64_t Emax;     // upper bound on directed edges: 2 n (K-1)
+    size_t status, D2, knn_idx, knn_d2, flag, eps, fwd_cnt, rev_cnt, fill_cnt, row_ptr;
+    size_t tmp_col, tmp_d2, col, w, d2e, deg, diag, rhs, P, Wadj, S, b, cgv, total;
+
+    explicit Layout(const gll_problem& p) {
+        n = p.n; d = p.d; base = p.base; C = p.C;
+        K = p.K < p.n ? p.K : p.n;
+        m = n - base;
+        ldD = (n + 3) & ~3;
+        Emax = 2LL * n * (K - 1);
+        size_t off = 0;
+        auto take = [&](size_t bytes) {
+            size_t at = off;
+            off += (bytes + 255) & ~size_t(255);
+            return at;
+        };
+        status = take(GLL_ST_NWORDS * 4);
+        D2 = take(size_t(n) * ldD * 4);
+        knn_idx = take(size_t(n) * K * 4);
+        knn_d2 = take(size_t(n) * K * 4);
+        flag = take(size_t(n) * K);
+        eps = take(size_t(n) * 4);
+        fwd_cnt = take(size_t(n) * 4);
+        rev_cnt = take(size_t(n) * 4);
+        fill_cnt = take(size_t(n) * 4);
+        row_ptr = take(size_t(n + 1) * 4);
+        tmp_col = take(size_t(Emax) * 4);
+        tmp_d2 = take(size_t(Emax) * 4);
+        col = take(size_t(Emax) * 4);
+        w = take(size_t(Emax) * 4);
+        d2e = take(size_t(Emax) * 4);
+        deg = take(size_t(n) * 4);
+        diag = take(size_t(m) * 4);
+        rhs = take(size_t(m) * C * 4);
+        P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)
+        Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
+        S = take(size_t(Emax) * 4);        // per-edge coefficient (auto eps only)
+        b = take(size_t(n) * 4);           // auto-eps b_i (GLL.py:126)
+        cgv = take(size_t(5) * m * C * 4); // CG vectors when they do not fit in LDS
+        total = off;
+    }
+    template <typename T>
+    T* at(void* ws, size_t o) const { return reinterpret_cast<T*>(static_cast<char*>(ws) + o); }
+};
+
+// ---------------------------------------------------------------------------------------
+// Device helpers
+// ---------------------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+template <typename T>
+__device__ __forceinline__ float to_f32(T v) { return static_cast<float>(v); }
+
+// Load 4 consecutive floats p[k..k+3] (zeros beyond `lim`).  VEC: 16-B vector load, needs
+// lim % 4 == 0 and 16-B alignment; otherwise scalar guarded loads.
+template <bool VEC>
+__device__ __forceinline__ f32x4 load4(const float* __restrict__ p, int k, int lim) {
+    f32x4 v;
+    if constexpr (VEC) {
+        if (k < lim) v = *reinterpret_cast<const f32x4*>(p + k);
+        else v = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+        v.x = (k + 0 < lim) ? p[k + 0] : 0.f;
+        v.y = (k + 1 < lim) ? p[k + 1] : 0.f;
+        v.z = (k + 2 < lim) ? p[k + 2] : 0.f;
+        v.w = (k + 3 < lim) ? p[k + 3] : 0.f;
+    }
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// Launchers (host side, one per translation unit)
+// ---------------------------------------------------------------------------------------
+void prof_begin(int kid, hipStream_t s);
+void prof_end(int kid, hipStream_t s);
+
+hipError_t launch_gram(const float* X, int n, int d, float* D2, int ldD, int32_t* status,
+                       bool vec, hipStream_t s);
+hipError_t launch_select(const float* D2, int ldD, const float* X, int n, int d, int K,
+                         float eps_fixed, bool auto_eps, int32_t* knn_idx, float* knn_d2,
+                         float* eps, int32_t* fwd_cnt, int32_t* rev_cnt, int32_t* fill_cnt,
+                         int32_t* status, bool vec, hipStream_t s);
+hipError_t launch_graph_build(const Layout& L, void* ws, hipStream_t s);
+hipError_t launch_finalize(const Layout& L, void* ws, const void* Y, int y_dtype, float tau,
+                           hipStream_t s);
+hipError_t launch_cg_luu(const Layout& L, void* ws, const void* b, int b_dtype, double* out64,
+                         float* out32, float rtol, int max_iter, int32_t* st_nonconv,
+                         int32_t* st_iters, hipStream_t s);
+hipError_t launch_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col,
+                         const float* val, const float* b, float* x, float atol, int max_iter,
+                         int32_t* iters, int32_t* nonconv, float* gvec, hipStream_t s);
+hipError_t launch_backward_grad(const Layout& L, void* ws, const float* X, bool auto_eps,
+                                float* gradX, bool vec, hipStream_t s);
+
+}  // namespace gll

@@ -1,0 +1,183 @@
+// grad.hip -- feature gradient of the Laplace-learning layer.
+//
+// Replaces the backward tail of /root/reference/GLL.py: the per-class loop over
+// graph.gradient (GLL.py:111-120), the self-tuning-eps term (GLL.py:124-139) and the
+// Laplacian SpMM laplacian(G o V) @ X (GLL.py:146-159), in closed form:
+//     G_ij = sum_c (w_ic - w_jc)(P_jc - P_ic),  V_ij = -8 W_ij / (eps_i eps_j),  S = G V
+//     grad_i = sum_j coef_ij (x_i - x_j)
+//     coef_ij = S_ij                                                  (fixed eps)
+//     coef_ij = S_ij - b_i [j = kth(i)] - b_j [kth(j) = i]            (auto eps)
+//     b_i = sum_j G_ij d_ij^2 V_ij / (2 eps_i^2)
+// Both kinds of extra term sit on graph edges (kth(i) is a neighbour of i), so the whole
+// backward is ONE pass over the CSR (fixed eps) or two (auto eps: b must be complete
+// before any row uses its neighbours' b).  One wave per row; lanes first own edges
+// (coefficients), then own feature columns (the x_j gathers, 16-B coalesced per lane).
+#include "gll_internal.h"
+
+namespace gll {
+
+struct EdgeArgs {
+    int n, base, C, K, d;
+    const int32_t* row_ptr;
+    const int32_t* col;
+    const float* w;       // W_ij
+    const float* d2;      // d_ij^2
+    const float* eps;
+    const float* P;       // n x C  [Y; U]
+    const float* Wadj;    // n x C  [0; Luu^-1 gbar]
+    const int32_t* knn_idx;
+    float* S;             // per-edge S (auto)
+    float* b;             // per-row b (auto)
+};
+
+// G_ij * V_ij for edge e = (i, j)
+__device__ __forceinline__ float edge_gv(const EdgeArgs& a, int i, int j, float we, float ei,
+                                         float& gout) {
+    const float* wi = a.Wadj + size_t(i) * a.C;
+    const float* wj = a.Wadj + size_t(j) * a.C;
+    const float* pi = a.P + size_t(i) * a.C;
+    const float* pj = a.P + size_t(j) * a.C;
+    float g = 0.f;
+    for (int c = 0; c < a.C; ++c) g += (wi[c] - wj[c]) * (pj[c] - pi[c]);
+    gout = g;
+    const float v = -8.f * we / (ei * a.eps[j]);   // GLL.py:217/234
+    return g * v;
+}
+
+// auto eps, pass 1: S_ij and b_i
+__global__ __launch_bounds__(256) void edge_coef_kernel(EdgeArgs a) {
+    const int lane = lane_id();
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const int beg = a.row_ptr[i], end = a.row_ptr[i + 1];
+    const float ei = a.eps[i];
+    float bpart = 0.f;
+    for (int e = beg + lane; e < end; e += kWave) {
+        float g;
+        const float s = edge_gv(a, i, a.col[e], a.w[e], ei, g);
+        a.S[e] = s;
+        bpart += s * a.d2[e];   // G d^2 V
+    }
+    bpart = wave_sum(bpart);
+    if (lane == 0) a.b[i] = bpart / (2.f * ei * ei);  // modV = d^2 V / (2 eps_i^2), GLL.py:218
+}
+
+// out_i = (sum_e coef_e) x_i - sum_e coef_e x_{col_e};  AUTO selects the coefficient form
+template <bool AUTO, int ND, bool VEC>
+__global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float* __restrict__ X,
+                                                        float* __restrict__ out) {
+    const int lane = lane_id();
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const int d = a.d;
+    const int beg = a.row_ptr[i], end = a.row_ptr[i + 1];
+    const float ei = a.eps[i];
+    int kth_i = 0;
+    float b_i = 0.f;
+    if constexpr (AUTO) {
+        kth_i = a.knn_idx[size_t(i) * a.K + a.K - 1];
+        b_i = a.b[i];
+    }
+    f32x4 acc[ND];
+#pragma unroll
+    for (int q = 0; q < ND; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float csum = 0.f;
+    for (int e0 = beg; e0 < end; e0 += kWave) {
+        // lanes own edges: coefficient of edge e0 + lane
+        const int e = e0 + lane;
+        float cf = 0.f;
+        int cj = i;
+        if (e < end) {
+            cj = a.col[e];
+            if constexpr (AUTO) {
+                cf = a.S[e];
+                if (cj == kth_i) cf -= b_i;
+                if (a.knn_idx[size_t(cj) * a.K + a.K - 1] == i) cf -= a.b[cj];
+            } else {
+                float g;
+                cf = edge_gv(a, i, cj, a.w[e], ei, g);
+            }
+        }
+        // lanes own feature columns: accumulate coef_e * x_j in edge order
+        const int cnt = min(kWave, end - e0);
+
+        for (int t = 0; t < cnt; ++t) {
+            const float s = readlane_f(cf, t);
+            const int j = readlane_i(cj, t);
+            csum += s;
+            const float* xj = X + size_t(j) * d;
+#pragma unroll
+            for (int q = 0; q < ND; ++q) {
+                const int k = 4 * lane + 4 * kWave * q;
+                const f32x4 v = load4<VEC>(xj, k, d);
+                acc[q] += s * v;
+            }
+        }
+    }
+    const float* xi = X + size_t(i) * d;
+    float* oi = out + size_t(i) * d;
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+        const int k = 4 * lane + 4 * kWave * q;
+        const f32x4 v = load4<VEC>(xi, k, d);
+        const f32x4 r = csum * v - acc[q];
+        if constexpr (VEC) {
+            if (k < d) *reinterpret_cast<f32x4*>(oi + k) = r;
+        } else {
+            if (k + 0 < d) oi[k + 0] = r.x;
+            if (k + 1 < d) oi[k + 1] = r.y;
+            if (k + 2 < d) oi[k + 2] = r.z;
+            if (k + 3 < d) oi[k + 3] = r.w;
+        }
+    }
+}
+
+template <bool AUTO, bool VEC>
+static hipError_t grad_nd(const EdgeArgs& a, const float* X, float* out, hipStream_t s) {
+    dim3 grid((a.n + 3) / 4);
+    const int nd = (a.d + 255) / 256;
+    if (nd <= 1) grad_spmm_kernel<AUTO, 1, VEC><<<grid, 256, 0, s>>>(a, X, out);
+    else if (nd <= 2) grad_spmm_kernel<AUTO, 2, VEC><<<grid, 256, 0, s>>>(a, X, out);
+    else if (nd <= 4) grad_spmm_kernel<AUTO, 4, VEC><<<grid, 256, 0, s>>>(a, X, out);
+    else if (nd <= 8) grad_spmm_kernel<AUTO, 8, VEC><<<grid, 256, 0, s>>>(a, X, out);
+    else if (nd <= 16) grad_spmm_kernel<AUTO, 16, VEC><<<grid, 256, 0, s>>>(a, X, out);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_backward_grad(const Layout& L, void* ws, const float* X, bool auto_eps,
+                                float* gradX, bool vec, hipStream_t s) {
+    EdgeArgs a;
+    a.n = L.n;
+    a.base = L.base;
+    a.C = L.C;
+    a.K = L.K;
+    a.d = L.d;
+    a.row_ptr = L.at<int32_t>(ws, L.row_ptr);
+    a.col = L.at<int32_t>(ws, L.col);
+    a.w = L.at<float>(ws, L.w);
+    a.d2 = L.at<float>(ws, L.d2e);
+    a.eps = L.at<float>(ws, L.eps);
+    a.P = L.at<float>(ws, L.P);
+    a.Wadj = L.at<float>(ws, L.Wadj);
+    a.knn_idx = L.at<int32_t>(ws, L.knn_idx);
+    a.S = L.at<float>(ws, L.S);
+    a.b = L.at<float>(ws, L.b);
+    hipError_t e;
+    if (auto_eps) {
+        prof_begin(GLL_K_EDGE, s);
+        edge_coef_kernel<<<(L.n + 3) / 4, 256, 0, s>>>(a);
+        prof_end(GLL_K_EDGE, s);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        prof_begin(GLL_K_GRAD, s);
+        e = vec ? grad_nd<true, true>(a, X, gradX, s) : grad_nd<true, false>(a, X, gradX, s);
+        prof_end(GLL_K_GRAD, s);
+    } else {
+        prof_begin(GLL_K_GRAD, s);
+        e = vec ? grad_nd<false, true>(a, X, gradX, s) : grad_nd<false, false>(a, X, gradX, s);
+        prof_end(GLL_K_GRAD, s);
+    }
+    return e;
+}
+
+}  // namespace gll

@@ -1,0 +1,132 @@
+/*
+ * gll.h -- C ABI of the MI355X (gfx950) Graph Learning Layer hot path.
+ *
+ * Drop-in boundary for `LaplaceLearningSparseHard.apply(X, label_matrix, tau, epsilon)`
+ * of jwcalder/GraphLearningLayer.  Each entry point names the reference interface it
+ * replaces (file:line in the reference snapshot).  Plain pointers and sizes only: device
+ * pointers are HIP device memory, `stream` is a hipStream_t passed as void*.  Row-major,
+ * fp32 features, int32 indices.  Inputs and outputs are caller-owned; the caller also owns
+ * one workspace block per call (size from gll_workspace_bytes) that carries the graph from
+ * gll_forward to gll_backward (the reference keeps the same state on `ctx`,
+ * GLL.py:69-70).  Nothing here synchronises the host; nothing allocates; every call is
+ * stream-ordered and reentrant per stream.  Return codes: 0 ok, < 0 error (no exceptions
+ * cross the ABI).
+ */
+#ifndef GLL_H
+#define GLL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GLL_OK 0
+#define GLL_ERR_INVALID_ARG (-1)
+#define GLL_ERR_UNSUPPORTED (-2)
+#define GLL_ERR_HIP (-3)
+
+/* dtype codes of label_matrix / grad_output (the reference accepts float32 and int64
+ * one-hot label matrices: FullySup.py:153, train_and_adversarial.py:712) */
+#define GLL_DT_F32 0
+#define GLL_DT_F64 1
+#define GLL_DT_I64 2
+
+/* status words the device writes into the workspace (read with gll_status_offset) */
+#define GLL_ST_TINY_EPS 0      /* eps_i < 1e-10 seen (GLL.py:240-241 warns) */
+#define GLL_ST_FWD_NONCONV 1   /* forward CG columns that hit max_iter */
+#define GLL_ST_FWD_ITERS 2     /* max forward CG iterations over columns */
+#define GLL_ST_BWD_NONCONV 3   /* adjoint CG columns that hit max_iter */
+#define GLL_ST_BWD_ITERS 4     /* max adjoint CG iterations over columns */
+#define GLL_ST_NWORDS 16
+
+typedef struct gll_problem {
+    int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */
+    int32_t d;        /* feature dimension */
+    int32_t base;     /* labeled rows = label_matrix.shape[0] (GLL.py:32) */
+    int32_t C;        /* classes = label_matrix.shape[1] */
+    int32_t K;        /* neighbours incl. self; the reference hard-codes 25 (GLL.py:27) */
+    int32_t max_iter; /* CG iteration cap per column; 0 => 1000 */
+    float tau;        /* diagonal regulariser of Luu (GLL.py:48) */
+    float eps;        /* > 0: fixed epsilon (GLL.py:226); <= 0: 'auto' (GLL.py:200-205) */
+    float rtol;       /* CG stop: ||r_c|| <= rtol ||b_c|| per column; 0 => 1e-6 */
+    int32_t flags;    /* reserved, 0 */
+} gll_problem;
+
+/* Bytes of device workspace one forward+backward pair needs. */
+size_t gll_workspace_bytes(const gll_problem* p);
+
+/* Replaces LaplaceLearningSparseHard.forward (GLL.py:14-73) incl. knn_sym_dist
+ * (GLL.py:180-244), csgraph.laplacian (GLL.py:29) and the spsolve of GLL.py:53.
+ * X: n x d fp32 (16-B aligned for the vector path), Y: base x C of y_dtype,
+ * U: m x C float64 output (the reference returns float64, GLL.py:66). */
+int gll_forward(const gll_problem* p, const float* X, const void* Y, int y_dtype,
+                void* workspace, double* U, void* stream);
+
+/* Replaces LaplaceLearningSparseHard.backward (GLL.py:76-177): adjoint solve (GLL.py:93),
+ * edge gradient loop (GLL.py:111-120), auto-eps term (GLL.py:124-139) and the Laplacian
+ * SpMM (GLL.py:146-159).  gbar: m x C of g_dtype; gradX: n x d fp32 output.
+ * `workspace` must be the block the matching gll_forward filled. */
+int gll_backward(const gll_problem* p, const float* X, const void* Y, int y_dtype,
+                 void* workspace, const void* gbar, int g_dtype, float* gradX, void* stream);
+
+/* Graph only (the device half of knn_sym_dist, GLL.py:180-244): kNN search, symmetric
+ * CSR, eps, weights and degrees into the workspace; no solve.  Requires p->base == 0
+ * (no labeled block; size the workspace for that problem).  Read the arrays with
+ * gll_workspace_view. */
+int gll_graph(const gll_problem* p, const float* X, void* workspace, void* stream);
+
+/* Device pointers of the arrays held in a workspace (for the host mirror and tests). */
+typedef struct gll_view {
+    int32_t* knn_idx;  /* n x K  neighbour indices, self first, ascending distance */
+    float* knn_d2;     /* n x K  squared distances (fp32, exact difference form)    */
+    float* eps;        /* n      epsilon_i                                           */
+    int32_t* row_ptr;  /* n + 1  CSR of the symmetric kNN graph (no diagonal)       */
+    int32_t* col;      /* E      column indices, ascending within a row             */
+    float* w;          /* E      W_ij = exp(-4 d_ij^2 / (eps_i eps_j))               */
+    float* d2;         /* E      d_ij^2                                              */
+    float* deg;        /* n      weighted degree                                     */
+    float* U32;        /* m x C  forward solution, fp32                              */
+    float* wadj;       /* m x C  adjoint solution (after gll_backward)               */
+    int32_t* status;   /* GLL_ST_NWORDS status words                                 */
+} gll_view;
+int gll_workspace_view(const gll_problem* p, void* workspace, gll_view* out);
+
+/* Multi-RHS Jacobi-preconditioned CG on a general SPD CSR matrix (device replacement of
+ * stable_conjgrad, GLL.py:247-276, as used by utils.laplace, utils.py:589).
+ * A: m x m CSR (row_ptr m+1, col, val) fp32; b, x: m x C row-major fp32 (x is output).
+ * Stops per column when ||r_c||_2 <= atol (absolute, like stable_conjgrad's tol) or
+ * max_iter.  `iters` (device int, may be NULL) receives the max iteration count,
+ * `nonconv` (device int, may be NULL) the columns that hit max_iter.  `workspace`
+ * (gll_cg_csr_workspace_bytes, may be NULL when 5 m floats fit in LDS) holds the Krylov
+ * vectors of large systems. */
+size_t gll_cg_csr_workspace_bytes(int m, int C);
+int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const float* val,
+               const float* b, float* x, float atol, int max_iter, int32_t* iters,
+               int32_t* nonconv, void* workspace, void* stream);
+
+/* Instrumentation for bench.py: when enabled, every launch of kernel `kid` is bracketed
+ * by HIP events on its stream; gll_prof_read synchronises those events and returns the
+ * summed milliseconds and the launch count, then clears them. */
+#define GLL_K_GRAM 0
+#define GLL_K_SELECT 1
+#define GLL_K_MUTUAL 2
+#define GLL_K_SCAN 3
+#define GLL_K_FILL 4
+#define GLL_K_FINALIZE 5
+#define GLL_K_CG 6
+#define GLL_K_EDGE 7
+#define GLL_K_GRAD 8
+#define GLL_K_COUNT 9
+int gll_prof_enable(int kid, int on);
+int gll_prof_read(int kid, double* ms_total, int* count);
+const char* gll_kernel_name(int kid);
+
+/* Human-readable message for a return code. */
+const char* gll_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GLL_H */

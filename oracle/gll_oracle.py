@@ -91,8 +91,14 @@ def forward(X, Y, tau=0.0, epsilon="auto", K=25, knn=None):
         ind, dist = knn_exact(X, K)
     else:
         ind = np.asarray(knn[0], dtype=np.int64)
-        dist = np.asarray(knn[1], dtype=np.float64) if knn[1] is not None else \
-            np.sqrt(np.sum((X[:, None, :] - X[ind]) ** 2, axis=2))
+        if knn[1] is not None:
+            dist = np.asarray(knn[1], dtype=np.float64)
+        else:  # exact float64 distances of the given pairs, row blocks to bound memory
+            dist = np.empty(ind.shape)
+            for r0 in range(0, n, 256):
+                blk = ind[r0:r0 + 256]
+                dist[r0:r0 + 256] = np.sqrt(np.sum(
+                    (X[r0:r0 + 256, None, :] - X[blk]) ** 2, axis=2))
     g = graph_from_knn(ind, dist, epsilon)
     W = g.csr(g.W)
     deg = np.asarray(W.sum(axis=1)).ravel()

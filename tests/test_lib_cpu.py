@@ -1,0 +1,120 @@
+"""CPU-side checks of the C ABI library and the host logic (no GPU calls)."""
+import ctypes as ct
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from graphlearninglayer_amd import _lib
+from graphlearninglayer_amd import GLL as G
+from graphlearninglayer_amd.synth import CONFIGS, one_hot, sha256, synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "gll.h")).read()
+    return sorted(set(re.findall(r"^\w[\w\s\*]*?\b(gll_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    lib = _lib.lib()
+    declared = header_functions()
+    assert len(declared) >= 10
+    assert set(declared) == set(_lib.EXPORTS)
+    for name in declared:
+        assert hasattr(lib, name), name
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_problem_struct_matches_header():
+    src = open(os.path.join(ROOT, "include", "gll.h")).read()
+    body = src[src.index("typedef struct gll_problem"):src.index("} gll_problem;")]
+    fields = re.findall(r"(int32_t|float)\s+(\w+);", body)
+    assert [f for _, f in fields] == [f for f, _ in _lib.Problem._fields_]
+    assert ct.sizeof(_lib.Problem) == 4 * len(fields)
+
+
+def test_view_struct_matches_header():
+    src = open(os.path.join(ROOT, "include", "gll.h")).read()
+    body = src[src.index("typedef struct gll_view"):src.index("} gll_view;")]
+    names = re.findall(r"\*\s*(\w+);", body)
+    assert names == [f for f, _ in _lib.View._fields_]
+
+
+def test_workspace_bytes_and_validation():
+    lib = _lib.lib()
+    p = G.make_problem(1000, 512, 500, 10, 10, 0.07, 1.0)
+    nb = lib.gll_workspace_bytes(ct.byref(p))
+    # dominated by the n x n squared-distance matrix
+    assert 1000 * 1000 * 4 < nb < 1000 * 1000 * 4 + 8 * 2**20
+    bad = G.make_problem(1000, 512, 500, 10, 10, 0.07, 1.0)
+    bad.K = 1
+    assert lib.gll_workspace_bytes(ct.byref(bad)) == 0
+    big_k = G.make_problem(1000, 512, 500, 10, 100, 0.07, 1.0)
+    assert lib.gll_workspace_bytes(ct.byref(big_k)) == 0   # K-1 > 64 unsupported
+    assert lib.gll_strerror(-2).decode().startswith("unsupported")
+
+
+def test_entry_points_reject_bad_arguments_without_touching_the_gpu():
+    lib = _lib.lib()
+    p = G.make_problem(100, 16, 50, 10, 5, 0.0, 1.0)
+    assert lib.gll_forward(ct.byref(p), None, None, 0, None, None, None) == -1
+    assert lib.gll_backward(ct.byref(p), None, None, 0, None, None, 0, None, None) == -1
+    assert lib.gll_graph(ct.byref(p), None, None, None) == -1
+    assert lib.gll_cg_csr(0, 1, None, None, None, None, None, 1e-6, 10, None, None, None,
+                          None) == -1
+    assert lib.gll_prof_enable(99, 1) == -1
+
+
+def test_kernel_names():
+    names = [_lib.kernel_name(k) for k in range(_lib.K_COUNT)]
+    assert names[_lib.K_GRAM] == "gram_d2_kernel"
+    assert names[_lib.K_CG] == "cg_luu_kernel"
+
+
+def test_eps_and_problem_mapping():
+    assert G._eps_value("auto") == 0.0
+    assert G._eps_value(1) == 1.0
+    with pytest.warns(UserWarning):
+        assert G._eps_value(0.0) > 0.0
+    with pytest.raises(ValueError):
+        G._eps_value("bogus")
+    p = G.make_problem(8, 4, 3, 2, k=25)
+    assert p.K == 8   # k clamped to n like np.minimum(knn_ind.shape[1], k), GLL.py:187
+
+
+def test_no_gpu_means_loud_failure():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    X = torch.zeros(10, 4)
+    Y = torch.zeros(5, 2)
+    with pytest.raises(RuntimeError, match="GPU"):
+        G.LaplaceLearningSparseHard.apply(X, Y, 0.0, 1.0)
+
+
+def test_synth_is_deterministic_and_unit_norm():
+    c = CONFIGS["plumbing"]
+    X1, l1 = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=3)
+    X2, l2 = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=3)
+    assert sha256(X1) == sha256(X2)
+    assert np.allclose(np.linalg.norm(X1, axis=1), 1.0, atol=1e-6)
+    assert (l1[: 10] == np.arange(10)).all()
+    Y = one_hot(l1[: c["base"]])
+    assert Y.shape == (64, 10) and (Y.sum(1) == 1).all()
+
+
+def test_product_package_never_imports_the_oracle():
+    pkg = os.path.join(ROOT, "graphlearninglayer_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert not re.search(r"^\s*(from|import)\s+oracle\b", src, flags=re.M), f
+                assert "oracle." not in src, f
