@@ -11,21 +11,29 @@
 // Luu is never materialised: row u (graph row i = base + u) is
 //     diag[u] * p_u - sum_{e in row i, col_e >= base} w_e * p_{col_e - base}
 // over the sorted CSR of the symmetric kNN graph (labeled columns first, so the U block of
-// a row is its tail [row_ptr[i] + split_i, row_ptr[i+1])).  When they fit, the vectors
-// (x, r, p, Ap, M^-1) and the U-part of the CSR (cols, weights) are staged in LDS.
+// a row is a suffix of the row).
+//
+// cg_reg_kernel (m <= 8192): the iteration is latency-bound, so everything a thread owns
+// stays in registers (x, r, p, Ap, M^-1, diag and the row's U-block bounds for R = m/NT
+// rows per thread); only p is published through LDS for the SpMV gathers, and the U-block
+// CSR (cols, weights) is staged in LDS when it fits.  The SpMV walks the R rows of a thread
+// in lock step (ELL-style slot loop) so R independent gather chains are in flight.  Dot
+// products are DPP wave reductions; with one wave per column (m <= 1024) an iteration has
+// no barrier at all.
+// cg_lds_kernel: vectors in LDS or global memory, for systems larger than that.
 #include "gll_internal.h"
 
 namespace gll {
 
+static constexpr size_t kLdsLimit = 160 * 1024;
+
+// Block-wide sum of two values; every thread gets the totals (fixed order -> deterministic).
 template <int NT>
-struct BlockRed {
-    static constexpr int NW = NT / kWave;
-    float* buf;   // 2 phases x 2 values x NW
-    int phase = 0;
-    __device__ __forceinline__ void sum2(float& a, float& b) {
-        a = wave_sum(a);
-        b = wave_sum(b);
-        float* q = buf + phase * 2 * NW;
+__device__ __forceinline__ void block_sum2(float& a, float& b, float* red, int& phase) {
+    wave_sum2_dpp(a, b);
+    if constexpr (NT > kWave) {
+        constexpr int NW = NT / kWave;
+        float* q = red + phase * 2 * NW;
         phase ^= 1;
         if (lane_id() == 0) {
             q[threadIdx.x >> 6] = a;
@@ -40,34 +48,23 @@ struct BlockRed {
             b += q[NW + w];
         }
     }
-};
+}
 
-// Vectors live in LDS when vec_in_lds (else in the workspace); the U-part of the CSR is
-// staged in LDS when it holds at most mat_cap entries (decided on the device: its size is
-// only known after the graph build).
-template <int NT, typename TB>
-__global__ __launch_bounds__(NT) void cg_luu_kernel(
+template <int NT, int R, typename TB>
+__global__ __launch_bounds__(NT) void cg_reg_kernel(
     int m, int C, int base, const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ wv, const float* __restrict__ diag, const TB* __restrict__ bsrc,
     double* __restrict__ out64, float* __restrict__ out32, float rtol, int max_iter,
-    float* __restrict__ gvec, int vec_in_lds, int mat_cap, int32_t* __restrict__ st_nonconv,
-    int32_t* __restrict__ st_iters) {
+    int mat_cap, int32_t* __restrict__ st_nonconv, int32_t* __restrict__ st_iters) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
-    BlockRed<NT> red{smem};
-    float* vbase = smem + 4 * BlockRed<NT>::NW;
-    if (!vec_in_lds) vbase = gvec + size_t(c) * 5 * m;
-    float* X_ = vbase;
-    float* R_ = vbase + m;
-    float* P_ = vbase + 2 * m;
-    float* A_ = vbase + 3 * m;
-    float* M_ = vbase + 4 * m;
-    // U-part of the CSR: positions [e0, e1) of the graph rows base..n-1
+    float* red = smem;                              // 4 * 16 floats
+    float* P_ = smem + 64;                          // m floats
     const int e0 = row_ptr[base];
     const int e1 = row_ptr[base + m];
     const bool matl = (e1 - e0) <= mat_cap;
-    int* lcol = reinterpret_cast<int*>(smem + 4 * BlockRed<NT>::NW + (vec_in_lds ? 5 * m : 0));
+    int* lcol = reinterpret_cast<int*>(P_ + ((m + 3) & ~3));
     float* lw = reinterpret_cast<float*>(lcol + (e1 - e0));
     if (matl) {
         for (int e = e0 + tid; e < e1; e += NT) {
@@ -75,13 +72,125 @@ __global__ __launch_bounds__(NT) void cg_luu_kernel(
             lw[e - e0] = wv[e];
         }
     }
-    // x0 = 0, r = b, z = M^-1 r, p = z
+    // per-thread rows u = tid + NT q
+    int st[R], len[R];
+    float x[R], r[R], p[R], ap[R], mi[R], dg[R];
+    float rz = 0.f, bb = 0.f;
+    int maxlen = 0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int u = tid + NT * q;
+        st[q] = 0;
+        len[q] = 0;
+        x[q] = r[q] = p[q] = ap[q] = mi[q] = dg[q] = 0.f;
+        if (u < m) {
+            const int i = base + u;
+            const int rb0 = row_ptr[i], rb1 = row_ptr[i + 1];
+            int s = rb0;
+            while (s < rb1 && col[s] < base) ++s;   // labeled columns are a prefix
+            st[q] = s - e0;
+            len[q] = rb1 - s;
+            maxlen = max(maxlen, len[q]);
+            dg[q] = diag[u];
+            mi[q] = dg[q] > 0.f ? 1.f / dg[q] : 0.f;
+            const float bu = to_f32(bsrc[size_t(u) * C + c]);
+            r[q] = mi[q] > 0.f ? bu : 0.f;          // zero-diagonal rows are decoupled: x = 0
+            p[q] = mi[q] * r[q];
+            P_[u] = p[q];
+            rz += r[q] * p[q];
+            bb += r[q] * r[q];
+        }
+    }
+    int phase = 0;
+    if constexpr (NT > kWave) __syncthreads();      // staged matrix + P_ visible block-wide
+    block_sum2<NT>(rz, bb, red, phase);
+    const float tol2 = rtol * rtol * bb;
+    int it = 0;
+    bool conv = !(bb > 0.f);
+    while (!conv && it < max_iter) {
+        ++it;
+        // Ap = diag p - W_uu p, R rows in lock step
+#pragma unroll
+        for (int q = 0; q < R; ++q) ap[q] = dg[q] * p[q];
+        if (matl) {
+            for (int s = 0; s < maxlen; ++s) {
+#pragma unroll
+                for (int q = 0; q < R; ++q)
+                    if (s < len[q]) ap[q] -= lw[st[q] + s] * P_[lcol[st[q] + s]];
+            }
+        } else {
+            for (int s = 0; s < maxlen; ++s) {
+#pragma unroll
+                for (int q = 0; q < R; ++q)
+                    if (s < len[q]) {
+                        const int e = e0 + st[q] + s;
+                        ap[q] -= wv[e] * P_[col[e] - base];
+                    }
+            }
+        }
+        float pap = 0.f, unused = 0.f;
+#pragma unroll
+        for (int q = 0; q < R; ++q) pap += p[q] * ap[q];
+        block_sum2<NT>(pap, unused, red, phase);
+        if (!(pap > 0.f)) break;   // breakdown or NaN: stop, reported as non-converged
+        const float alpha = rz / pap;
+        float rr = 0.f, rzn = 0.f;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            x[q] += alpha * p[q];
+            r[q] -= alpha * ap[q];
+            rr += r[q] * r[q];
+            rzn += r[q] * mi[q] * r[q];
+        }
+        block_sum2<NT>(rr, rzn, red, phase);
+        if (rr <= tol2) {
+            conv = true;
+            break;
+        }
+        const float beta = rzn / rz;
+        rz = rzn;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            p[q] = mi[q] * r[q] + beta * p[q];
+            const int u = tid + NT * q;
+            if (u < m) P_[u] = p[q];
+        }
+        if constexpr (NT > kWave) __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int u = tid + NT * q;
+        if (u < m) {
+            if (out64) out64[size_t(u) * C + c] = double(x[q]);
+            if (out32) out32[size_t(u) * C + c] = x[q];
+        }
+    }
+    if (tid == 0) {
+        if (st_iters) atomicMax(st_iters, it);
+        if (!conv && st_nonconv) atomicAdd(st_nonconv, 1);
+    }
+}
+
+// Large systems: vectors in LDS (<= 160 KiB) or in the workspace.
+template <int NT, typename TB>
+__global__ __launch_bounds__(NT) void cg_lds_kernel(
+    int m, int C, int base, const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ wv, const float* __restrict__ diag, const TB* __restrict__ bsrc,
+    double* __restrict__ out64, float* __restrict__ out32, float rtol, int max_iter,
+    float* __restrict__ gvec, int vec_in_lds, int32_t* __restrict__ st_nonconv,
+    int32_t* __restrict__ st_iters) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int c = blockIdx.x;
+    const int tid = threadIdx.x;
+    float* red = smem;
+    float* vb = vec_in_lds ? smem + 64 : gvec + size_t(c) * 5 * m;
+    float *X_ = vb, *R_ = vb + m, *P_ = vb + 2 * m, *A_ = vb + 3 * m, *M_ = vb + 4 * m;
     float rz = 0.f, bb = 0.f;
     for (int u = tid; u < m; u += NT) {
         const float dg = diag[u];
         const float mi = dg > 0.f ? 1.f / dg : 0.f;
         const float bu = to_f32(bsrc[size_t(u) * C + c]);
-        const float rb = mi > 0.f ? bu : 0.f;  // rows with zero diagonal are decoupled: x = 0
+        const float rb = mi > 0.f ? bu : 0.f;
         X_[u] = 0.f;
         R_[u] = rb;
         M_[u] = mi;
@@ -89,39 +198,29 @@ __global__ __launch_bounds__(NT) void cg_luu_kernel(
         rz += rb * mi * rb;
         bb += rb * rb;
     }
-    red.sum2(rz, bb);  // includes the barrier that publishes the LDS vectors/matrix
+    int phase = 0;
+    __syncthreads();
+    block_sum2<NT>(rz, bb, red, phase);
     const float tol2 = rtol * rtol * bb;
     int it = 0;
-    bool conv = bb <= tol2 || bb == 0.f;
+    bool conv = !(bb > 0.f);
     while (!conv && it < max_iter) {
         ++it;
-        // Ap and p.Ap
-        float pap = 0.f, dummy = 0.f;
+        float pap = 0.f, unused = 0.f;
         for (int u = tid; u < m; u += NT) {
             const int i = base + u;
-            const int rb0 = row_ptr[i], rb1 = row_ptr[i + 1];
             float acc = 0.f;
-            if (matl) {
-                // the U part is the tail of the sorted row; scan back from the end
-                for (int e = rb1 - 1; e >= rb0; --e) {
-                    const int j = lcol[e - e0];
-                    if (j < 0) break;
-                    acc += lw[e - e0] * P_[j];
-                }
-            } else {
-                for (int e = rb1 - 1; e >= rb0; --e) {
-                    const int j = col[e] - base;
-                    if (j < 0) break;
-                    acc += wv[e] * P_[j];
-                }
+            for (int e = row_ptr[i + 1] - 1; e >= row_ptr[i]; --e) {
+                const int j = col[e] - base;
+                if (j < 0) break;
+                acc += wv[e] * P_[j];
             }
-            const float pu = P_[u];
-            const float ap = diag[u] * pu - acc;
+            const float ap = diag[u] * P_[u] - acc;
             A_[u] = ap;
-            pap += pu * ap;
+            pap += P_[u] * ap;
         }
-        red.sum2(pap, dummy);
-        if (!(pap > 0.f)) break;  // breakdown (or NaN): stop, report non-convergence
+        block_sum2<NT>(pap, unused, red, phase);
+        if (!(pap > 0.f)) break;
         const float alpha = rz / pap;
         float rr = 0.f, rzn = 0.f;
         for (int u = tid; u < m; u += NT) {
@@ -131,7 +230,7 @@ __global__ __launch_bounds__(NT) void cg_luu_kernel(
             rr += ru * ru;
             rzn += ru * M_[u] * ru;
         }
-        red.sum2(rr, rzn);
+        block_sum2<NT>(rr, rzn, red, phase);
         if (rr <= tol2) {
             conv = true;
             break;
@@ -142,9 +241,8 @@ __global__ __launch_bounds__(NT) void cg_luu_kernel(
         __syncthreads();
     }
     for (int u = tid; u < m; u += NT) {
-        const float xu = X_[u];
-        if (out64) out64[size_t(u) * C + c] = double(xu);
-        if (out32) out32[size_t(u) * C + c] = xu;
+        if (out64) out64[size_t(u) * C + c] = double(X_[u]);
+        if (out32) out32[size_t(u) * C + c] = X_[u];
     }
     if (tid == 0) {
         if (st_iters) atomicMax(st_iters, it);
@@ -152,31 +250,24 @@ __global__ __launch_bounds__(NT) void cg_luu_kernel(
     }
 }
 
-static constexpr size_t kLdsLimit = 160 * 1024;
-static constexpr size_t kRedBytes = 4 * 16 * sizeof(float);
-
-template <int NT, typename TB>
-static hipError_t run_cg(const Layout& L, void* ws, const TB* b, double* out64, float* out32,
-                         float rtol, int max_iter, int32_t* st_nonconv, int32_t* st_iters,
-                         hipStream_t s) {
+template <int NT, int R, typename TB>
+static hipError_t run_reg(const Layout& L, void* ws, const TB* b, double* out64, float* out32,
+                          float rtol, int max_iter, int32_t* st_nonconv, int32_t* st_iters,
+                          hipStream_t s) {
     const int m = L.m;
-    const size_t vec_bytes = size_t(5) * m * sizeof(float);
-    const bool vec_lds = kRedBytes + vec_bytes <= kLdsLimit;
-    size_t lds = kRedBytes + (vec_lds ? vec_bytes : 0);
-    // entries of the graph rows >= base: m(K-1) forward + at most n(K-1) reverse
+    size_t lds = 64 * 4 + size_t((m + 3) & ~3) * 4;
+    // U-block entries: m(K-1) forward + at most n(K-1) reverse
     const int64_t eu_bound = int64_t(m + L.n) * (L.K - 1);
     int64_t cap = int64_t(kLdsLimit - lds) / 8;
     if (cap > eu_bound) cap = eu_bound;
     if (cap < 0) cap = 0;
     lds += size_t(cap) * 8;
-    auto fn = cg_luu_kernel<NT, TB>;
+    auto fn = cg_reg_kernel<NT, R, TB>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-    fn<<<L.C, NT, lds, s>>>(m, L.C, L.base, L.at<int32_t>(ws, L.row_ptr),
-                            L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
-                            L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter,
-                            L.at<float>(ws, L.cgv), vec_lds ? 1 : 0, int(cap), st_nonconv,
-                            st_iters);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    fn<<<L.C, NT, lds, s>>>(m, L.C, L.base, L.at<int32_t>(ws, L.row_ptr), L.at<int32_t>(ws, L.col),
+                            L.at<float>(ws, L.w), L.at<float>(ws, L.diag), b, out64, out32, rtol,
+                            max_iter, int(cap), st_nonconv, st_iters);
     return hipGetLastError();
 }
 
@@ -184,9 +275,28 @@ template <typename TB>
 static hipError_t cg_dispatch(const Layout& L, void* ws, const TB* b, double* out64,
                               float* out32, float rtol, int max_iter, int32_t* st_nonconv,
                               int32_t* st_iters, hipStream_t s) {
-    if (L.m <= 2048)
-        return run_cg<256, TB>(L, ws, b, out64, out32, rtol, max_iter, st_nonconv, st_iters, s);
-    return run_cg<1024, TB>(L, ws, b, out64, out32, rtol, max_iter, st_nonconv, st_iters, s);
+    const int m = L.m;
+#define GLL_REG(NT, R) \
+    return run_reg<NT, R, TB>(L, ws, b, out64, out32, rtol, max_iter, st_nonconv, st_iters, s)
+    if (m <= 64 * 2) GLL_REG(64, 2);
+    if (m <= 64 * 4) GLL_REG(64, 4);
+    if (m <= 64 * 8) GLL_REG(64, 8);
+    if (m <= 64 * 16) GLL_REG(64, 16);
+    if (m <= 256 * 8) GLL_REG(256, 8);
+    if (m <= 256 * 16) GLL_REG(256, 16);
+    if (m <= 1024 * 8) GLL_REG(1024, 8);
+#undef GLL_REG
+    const size_t vec_bytes = size_t(5) * m * sizeof(float);
+    const bool vec_lds = 64 * 4 + vec_bytes <= kLdsLimit;
+    const size_t lds = 64 * 4 + (vec_lds ? vec_bytes : 0);
+    auto fn = cg_lds_kernel<1024, TB>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    fn<<<L.C, 1024, lds, s>>>(m, L.C, L.base, L.at<int32_t>(ws, L.row_ptr),
+                              L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
+                              L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter,
+                              L.at<float>(ws, L.cgv), vec_lds ? 1 : 0, st_nonconv, st_iters);
+    return hipGetLastError();
 }
 
 hipError_t launch_cg_luu(const Layout& L, void* ws, const void* b, int b_dtype, double* out64,
@@ -222,8 +332,8 @@ __global__ __launch_bounds__(NT) void cg_csr_kernel(int m, int C, const int32_t*
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
-    BlockRed<NT> red{smem};
-    float* vb = vec_in_lds ? smem + 4 * BlockRed<NT>::NW : gvec + size_t(c) * 5 * m;
+    float* red = smem;
+    float* vb = vec_in_lds ? smem + 64 : gvec + size_t(c) * 5 * m;
     float *X_ = vb, *R_ = vb + m, *P_ = vb + 2 * m, *A_ = vb + 3 * m, *M_ = vb + 4 * m;
     float rz = 0.f, rr0 = 0.f;
     for (int u = tid; u < m; u += NT) {
@@ -239,20 +349,22 @@ __global__ __launch_bounds__(NT) void cg_csr_kernel(int m, int C, const int32_t*
         rz += bu * mi * bu;
         rr0 += bu * bu;
     }
-    red.sum2(rz, rr0);
+    int phase = 0;
+    __syncthreads();
+    block_sum2<NT>(rz, rr0, red, phase);
     const float tol2 = atol * atol;
     int it = 0;
     bool conv = rr0 <= tol2;
     while (!conv && it < max_iter) {
         ++it;
-        float pap = 0.f, dummy = 0.f;
+        float pap = 0.f, unused = 0.f;
         for (int u = tid; u < m; u += NT) {
             float acc = 0.f;
             for (int e = rp[u]; e < rp[u + 1]; ++e) acc += val[e] * P_[col[e]];
             A_[u] = acc;
             pap += P_[u] * acc;
         }
-        red.sum2(pap, dummy);
+        block_sum2<NT>(pap, unused, red, phase);
         if (!(pap > 0.f)) break;
         const float alpha = rz / pap;
         float rr = 0.f, rzn = 0.f;
@@ -263,7 +375,7 @@ __global__ __launch_bounds__(NT) void cg_csr_kernel(int m, int C, const int32_t*
             rr += ru * ru;
             rzn += ru * M_[u] * ru;
         }
-        red.sum2(rr, rzn);
+        block_sum2<NT>(rr, rzn, red, phase);
         if (rr <= tol2) {
             conv = true;
             break;
@@ -284,12 +396,12 @@ hipError_t launch_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* co
                          const float* val, const float* b, float* x, float atol, int max_iter,
                          int32_t* iters, int32_t* nonconv, float* gvec, hipStream_t s) {
     const size_t vec_bytes = size_t(5) * m * sizeof(float);
-    const bool vec_lds = kRedBytes + vec_bytes <= kLdsLimit;
+    const bool vec_lds = 64 * 4 + vec_bytes <= kLdsLimit;
     if (!vec_lds && gvec == nullptr) return hipErrorInvalidValue;
-    const size_t lds = kRedBytes + (vec_lds ? vec_bytes : 0);
+    const size_t lds = 64 * 4 + (vec_lds ? vec_bytes : 0);
     auto fn = cg_csr_kernel<256>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
     prof_begin(GLL_K_CG, s);
     fn<<<C, 256, lds, s>>>(m, C, row_ptr, col, val, b, x, atol, max_iter, gvec, vec_lds ? 1 : 0,
                            iters, nonconv);

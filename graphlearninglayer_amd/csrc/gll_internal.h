@@ -86,6 +86,36 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 }
 __device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
+// Wave64 sum through DPP (no LDS round trips): quad butterflies, half-row and row mirrors,
+// then row_bcast15/31 carry the row sums up to lane 63, which is broadcast via readlane.
+// Fixed combination order -> deterministic; the result is wave-uniform (scalar).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_add(float v) {
+    const int s = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf,
+                                              false);
+    return v + __builtin_bit_cast(float, s);
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v = dpp_add<0xB1, 0xf>(v);    // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E, 0xf>(v);    // quad_perm [2,3,0,1]
+    v = dpp_add<0x141, 0xf>(v);   // row_half_mirror
+    v = dpp_add<0x140, 0xf>(v);   // row_mirror
+    v = dpp_add<0x142, 0xa>(v);   // row_bcast15 -> rows 1, 3
+    v = dpp_add<0x143, 0xc>(v);   // row_bcast31 -> rows 2, 3
+    return readlane_f(v, 63);
+}
+// two independent sums interleaved (ILP across the two DPP chains)
+__device__ __forceinline__ void wave_sum2_dpp(float& a, float& b) {
+    a = dpp_add<0xB1, 0xf>(a); b = dpp_add<0xB1, 0xf>(b);
+    a = dpp_add<0x4E, 0xf>(a); b = dpp_add<0x4E, 0xf>(b);
+    a = dpp_add<0x141, 0xf>(a); b = dpp_add<0x141, 0xf>(b);
+    a = dpp_add<0x140, 0xf>(a); b = dpp_add<0x140, 0xf>(b);
+    a = dpp_add<0x142, 0xa>(a); b = dpp_add<0x142, 0xa>(b);
+    a = dpp_add<0x143, 0xc>(a); b = dpp_add<0x143, 0xc>(b);
+    a = readlane_f(a, 63);
+    b = readlane_f(b, 63);
+}
+
 template <typename T>
 __device__ __forceinline__ float to_f32(T v) { return static_cast<float>(v); }
 

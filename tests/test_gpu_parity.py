@@ -125,8 +125,10 @@ def test_cpu_tensor_input_roundtrips_to_cpu():
 def test_float64_and_noncontiguous_features():
     GLL = _gll()
     c = Case("plumbing_epsauto_tau0p07_f32")
-    Xb = torch.from_numpy(np.concatenate([c.X, c.X], axis=1)).cuda()
-    X = Xb[:, ::2].double().requires_grad_(True)   # strided view, float64
+    wide = np.zeros((c.X.shape[0], 2 * c.X.shape[1]))
+    wide[:, ::2] = c.X
+    X = torch.from_numpy(wide).cuda()[:, ::2].requires_grad_(True)   # strided float64 view
+    assert not X.is_contiguous()
     U = GLL.LaplaceLearningSparseHard.apply(X, torch.from_numpy(c.Y).cuda(), c.tau, c.eps, c.k)
     U.backward(torch.from_numpy(c.gbar).cuda())
     assert X.grad.dtype == torch.float64

@@ -17,4 +17,21 @@ STEPS=${STEPS:-smoke,tests,bench}
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *tests* ]] && run tests 900 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-}
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 20 ${BENCH_ARGS:-}
+if [[ $STEPS == *prof* ]]; then
+  export TMPDIR=/tmp
+  R=$PWD
+  PROF_CFG=${PROF_CFG:-ns}
+  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$PROF_CFG" -o run -- \
+      python3 "$R/bench.py" --config $PROF_CFG --steps ${PROF_STEPS:-100} --warmup 10 --cpu-seconds 0 --no-profile
+  find "$R/gpurun_out/prof_$PROF_CFG" -name '*kernel_stats.csv' -exec cat {} \; | head -30
+fi
+if [[ $STEPS == *pmc* ]]; then
+  export TMPDIR=/tmp
+  R=$PWD
+  PROF_CFG=${PROF_CFG:-ns}
+  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_fetch_$PROF_CFG" -o run -- \
+      python3 "$R/bench.py" --config $PROF_CFG --steps 20 --warmup 5 --cpu-seconds 0 --no-profile
+  run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_write_$PROF_CFG" -o run -- \
+      python3 "$R/bench.py" --config $PROF_CFG --steps 20 --warmup 5 --cpu-seconds 0 --no-profile
+fi
 exit 0
