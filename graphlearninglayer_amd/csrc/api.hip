@@ -38,7 +38,7 @@ void prof_begin(int kid, hipStream_t s) {
     std::lock_guard<std::mutex> lk(g_prof.mu);
     hipEvent_t e = g_prof.get();
     if (!e) return;
-    hipEventRecord(e, s);
+    (void)hipEventRecord(e, s);
     g_prof.pending[kid].push_back(e);
 }
 
@@ -52,7 +52,7 @@ void prof_end(int kid, hipStream_t s) {
         g_prof.pending[kid].pop_back();
         return;
     }
-    hipEventRecord(e, s);
+    (void)hipEventRecord(e, s);
     g_prof.pending[kid].push_back(e);
 }
 

@@ -20,7 +20,7 @@ struct Layout {
     int ldD;          // leading dimension of the n x n squared-distance matrix
     int64_t Emax;     // upper bound on directed edges: 2 n (K-1)
     size_t status, D2, knn_idx, knn_d2, flag, eps, fwd_cnt, rev_cnt, fill_cnt, row_ptr;
-    size_t tmp_col, tmp_d2, col, w, d2e, deg, diag, rhs, P, Wadj, S, b, cgv, total;
+    size_t tmp_col, tmp_d2, col, w, d2e, deg, ucnt, diag, rhs, P, Wadj, S, b, cgv, total;
 
     explicit Layout(const gll_problem& p) {
         n = p.n; d = p.d; base = p.base; C = p.C;
@@ -50,6 +50,7 @@ struct Layout {
         w = take(size_t(Emax) * 4);
         d2e = take(size_t(Emax) * 4);
         deg = take(size_t(n) * 4);
+        ucnt = take(size_t(m) * 4);        // U-block entries per unlabeled row
         diag = take(size_t(m) * 4);
         rhs = take(size_t(m) * C * 4);
         P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)

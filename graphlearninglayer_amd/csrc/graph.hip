@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void row_finalize_kernel(
     const float* __restrict__ eps, const TY* __restrict__ Y, int32_t* __restrict__ col,
     float* __restrict__ w, float* __restrict__ d2e, float* __restrict__ deg,
     float* __restrict__ diag, float* __restrict__ rhs, float* __restrict__ P,
-    float* __restrict__ Wadj) {
+    float* __restrict__ Wadj, int32_t* __restrict__ ucnt) {
     __shared__ int s_col[4][kRowChunk];
     __shared__ float s_d2[4][kRowChunk];
     __shared__ float s_w[4][kRowChunk];
@@ -117,6 +117,7 @@ __global__ __launch_bounds__(256) void row_finalize_kernel(
     const float ei = eps[i];
 
     float dsum = 0.f;
+    int nlab = 0;
     float racc[kMaxCPerLane];
 #pragma unroll
     for (int q = 0; q < kMaxCPerLane; ++q) racc[q] = 0.f;
@@ -146,6 +147,7 @@ __global__ __launch_bounds__(256) void row_finalize_kernel(
             w[beg + e] = we;
             s_w[wv][e - lo] = we;
             dsum += we;
+            nlab += c < base ? 1 : 0;
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -182,7 +184,11 @@ __global__ __launch_bounds__(256) void row_finalize_kernel(
             }
         }
     }
-    if (i >= base && lane == 0) diag[i - base] = dsum + tau;   // Luu + tau I (GLL.py:48)
+    nlab = wave_sum_i(nlab);
+    if (i >= base && lane == 0) {
+        diag[i - base] = dsum + tau;   // Luu + tau I (GLL.py:48)
+        ucnt[i - base] = L - nlab;     // the U block is the row's sorted suffix
+    }
 }
 
 hipError_t launch_graph_build(const Layout& L, void* ws, hipStream_t s) {
@@ -217,7 +223,7 @@ hipError_t launch_finalize(const Layout& L, void* ws, const void* Y, int y_dtype
         L.at<float>(ws, L.tmp_d2), L.at<float>(ws, L.eps), static_cast<const T*>(Y),           \
         L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w), L.at<float>(ws, L.d2e),                \
         L.at<float>(ws, L.deg), L.at<float>(ws, L.diag), L.at<float>(ws, L.rhs),               \
-        L.at<float>(ws, L.P), L.at<float>(ws, L.Wadj))
+        L.at<float>(ws, L.P), L.at<float>(ws, L.Wadj), L.at<int32_t>(ws, L.ucnt))
     prof_begin(GLL_K_FINALIZE, s);
     if (y_dtype == GLL_DT_F32) GLL_FIN(float);
     else if (y_dtype == GLL_DT_F64) GLL_FIN(double);

@@ -13,13 +13,12 @@
 // over the sorted CSR of the symmetric kNN graph (labeled columns first, so the U block of
 // a row is a suffix of the row).
 //
-// cg_reg_kernel (m <= 8192): the iteration is latency-bound, so everything a thread owns
-// stays in registers (x, r, p, Ap, M^-1, diag and the row's U-block bounds for R = m/NT
-// rows per thread); only p is published through LDS for the SpMV gathers, and the U-block
-// CSR (cols, weights) is staged in LDS when it fits.  The SpMV walks the R rows of a thread
-// in lock step (ELL-style slot loop) so R independent gather chains are in flight.  Dot
-// products are DPP wave reductions; with one wave per column (m <= 1024) an iteration has
-// no barrier at all.
+// cg_ell_kernel (m <= 4096): the iteration is latency-bound, so a thread owns R rows and
+// keeps everything about them in registers: x, r, p, Ap, M^-1, diag AND the first S
+// entries of each row's U block as an ELL slice (column, weight), zero-padded so the SpMV
+// gathers are branch-free and all S are in flight at once (entries beyond S are read from
+// the CSR).  Only p is published through LDS for the gathers.  Dot products are DPP wave
+// reductions plus one LDS exchange across waves; an iteration has three barriers.
 // cg_lds_kernel: vectors in LDS or global memory, for systems larger than that.
 #include "gll_internal.h"
 
@@ -50,51 +49,48 @@ __device__ __forceinline__ void block_sum2(float& a, float& b, float* red, int& 
     }
 }
 
-template <int NT, int R, typename TB>
-__global__ __launch_bounds__(NT) void cg_reg_kernel(
-    int m, int C, int base, const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-    const float* __restrict__ wv, const float* __restrict__ diag, const TB* __restrict__ bsrc,
-    double* __restrict__ out64, float* __restrict__ out32, float rtol, int max_iter,
-    int mat_cap, int32_t* __restrict__ st_nonconv, int32_t* __restrict__ st_iters) {
+
+template <int NT, int R, int S, typename TB>
+__global__ __launch_bounds__(NT) void cg_ell_kernel(
+    int m, int C, int base, const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ ucnt,
+    const int32_t* __restrict__ col, const float* __restrict__ wv, const float* __restrict__ diag,
+    const TB* __restrict__ bsrc, double* __restrict__ out64, float* __restrict__ out32,
+    float rtol, int max_iter, int32_t* __restrict__ st_nonconv, int32_t* __restrict__ st_iters) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
-    float* red = smem;                              // 4 * 16 floats
-    float* P_ = smem + 64;                          // m floats
-    const int e0 = row_ptr[base];
-    const int e1 = row_ptr[base + m];
-    const bool matl = (e1 - e0) <= mat_cap;
-    int* lcol = reinterpret_cast<int*>(P_ + ((m + 3) & ~3));
-    float* lw = reinterpret_cast<float*>(lcol + (e1 - e0));
-    if (matl) {
-        for (int e = e0 + tid; e < e1; e += NT) {
-            lcol[e - e0] = col[e] - base;
-            lw[e - e0] = wv[e];
-        }
-    }
-    // per-thread rows u = tid + NT q
-    int st[R], len[R];
+    float* red = smem;        // 4 x 16 floats of reduction scratch
+    float* P_ = smem + 64;    // search direction, gathered by every thread
+    int ec[R][S];
+    float ew[R][S];
+    int ost[R], olen[R];
     float x[R], r[R], p[R], ap[R], mi[R], dg[R];
     float rz = 0.f, bb = 0.f;
-    int maxlen = 0;
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int u = tid + NT * q;
-        st[q] = 0;
-        len[q] = 0;
+        int len = 0, st = 0;
         x[q] = r[q] = p[q] = ap[q] = mi[q] = dg[q] = 0.f;
         if (u < m) {
-            const int i = base + u;
-            const int rb0 = row_ptr[i], rb1 = row_ptr[i + 1];
-            int s = rb0;
-            while (s < rb1 && col[s] < base) ++s;   // labeled columns are a prefix
-            st[q] = s - e0;
-            len[q] = rb1 - s;
-            maxlen = max(maxlen, len[q]);
+            len = ucnt[u];
+            st = row_ptr[base + u + 1] - len;
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) {   // ELL slice: independent loads, padded with (0, 0)
+            const bool live = s < len;
+            const int e = live ? st + s : 0;
+            const int cc = col[e] - base;
+            const float ww = wv[e];
+            ec[q][s] = live ? cc : 0;
+            ew[q][s] = live ? ww : 0.f;
+        }
+        ost[q] = st + S;
+        olen[q] = len - S;
+        if (u < m) {
             dg[q] = diag[u];
             mi[q] = dg[q] > 0.f ? 1.f / dg[q] : 0.f;
             const float bu = to_f32(bsrc[size_t(u) * C + c]);
-            r[q] = mi[q] > 0.f ? bu : 0.f;          // zero-diagonal rows are decoupled: x = 0
+            r[q] = mi[q] > 0.f ? bu : 0.f;   // zero-diagonal rows are decoupled: x = 0
             p[q] = mi[q] * r[q];
             P_[u] = p[q];
             rz += r[q] * p[q];
@@ -102,35 +98,26 @@ __global__ __launch_bounds__(NT) void cg_reg_kernel(
         }
     }
     int phase = 0;
-    if constexpr (NT > kWave) __syncthreads();      // staged matrix + P_ visible block-wide
+    if constexpr (NT > kWave) __syncthreads();
     block_sum2<NT>(rz, bb, red, phase);
     const float tol2 = rtol * rtol * bb;
     int it = 0;
     bool conv = !(bb > 0.f);
     while (!conv && it < max_iter) {
         ++it;
-        // Ap = diag p - W_uu p, R rows in lock step
-#pragma unroll
-        for (int q = 0; q < R; ++q) ap[q] = dg[q] * p[q];
-        if (matl) {
-            for (int s = 0; s < maxlen; ++s) {
-#pragma unroll
-                for (int q = 0; q < R; ++q)
-                    if (s < len[q]) ap[q] -= lw[st[q] + s] * P_[lcol[st[q] + s]];
-            }
-        } else {
-            for (int s = 0; s < maxlen; ++s) {
-#pragma unroll
-                for (int q = 0; q < R; ++q)
-                    if (s < len[q]) {
-                        const int e = e0 + st[q] + s;
-                        ap[q] -= wv[e] * P_[col[e] - base];
-                    }
-            }
-        }
         float pap = 0.f, unused = 0.f;
 #pragma unroll
-        for (int q = 0; q < R; ++q) pap += p[q] * ap[q];
+        for (int q = 0; q < R; ++q) {
+            float acc = 0.f;
+#pragma unroll
+            for (int s = 0; s < S; ++s) acc += ew[q][s] * P_[ec[q][s]];
+            for (int t = 0; t < olen[q]; ++t) {
+                const int e = ost[q] + t;
+                acc += wv[e] * P_[col[e] - base];
+            }
+            ap[q] = dg[q] * p[q] - acc;   // (Luu p)_u = (deg_u + tau) p_u - sum_j W_uj p_j
+            pap += p[q] * ap[q];
+        }
         block_sum2<NT>(pap, unused, red, phase);
         if (!(pap > 0.f)) break;   // breakdown or NaN: stop, reported as non-converged
         const float alpha = rz / pap;
@@ -250,24 +237,16 @@ __global__ __launch_bounds__(NT) void cg_lds_kernel(
     }
 }
 
-template <int NT, int R, typename TB>
-static hipError_t run_reg(const Layout& L, void* ws, const TB* b, double* out64, float* out32,
+
+template <int NT, int R, int S, typename TB>
+static hipError_t run_ell(const Layout& L, void* ws, const TB* b, double* out64, float* out32,
                           float rtol, int max_iter, int32_t* st_nonconv, int32_t* st_iters,
                           hipStream_t s) {
-    const int m = L.m;
-    size_t lds = 64 * 4 + size_t((m + 3) & ~3) * 4;
-    // U-block entries: m(K-1) forward + at most n(K-1) reverse
-    const int64_t eu_bound = int64_t(m + L.n) * (L.K - 1);
-    int64_t cap = int64_t(kLdsLimit - lds) / 8;
-    if (cap > eu_bound) cap = eu_bound;
-    if (cap < 0) cap = 0;
-    lds += size_t(cap) * 8;
-    auto fn = cg_reg_kernel<NT, R, TB>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-    fn<<<L.C, NT, lds, s>>>(m, L.C, L.base, L.at<int32_t>(ws, L.row_ptr), L.at<int32_t>(ws, L.col),
-                            L.at<float>(ws, L.w), L.at<float>(ws, L.diag), b, out64, out32, rtol,
-                            max_iter, int(cap), st_nonconv, st_iters);
+    const size_t lds = 64 * 4 + size_t((L.m + 3) & ~3) * 4;
+    cg_ell_kernel<NT, R, S, TB><<<L.C, NT, lds, s>>>(
+        L.m, L.C, L.base, L.at<int32_t>(ws, L.row_ptr), L.at<int32_t>(ws, L.ucnt),
+        L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w), L.at<float>(ws, L.diag), b, out64, out32,
+        rtol, max_iter, st_nonconv, st_iters);
     return hipGetLastError();
 }
 
@@ -276,16 +255,16 @@ static hipError_t cg_dispatch(const Layout& L, void* ws, const TB* b, double* ou
                               float* out32, float rtol, int max_iter, int32_t* st_nonconv,
                               int32_t* st_iters, hipStream_t s) {
     const int m = L.m;
-#define GLL_REG(NT, R) \
-    return run_reg<NT, R, TB>(L, ws, b, out64, out32, rtol, max_iter, st_nonconv, st_iters, s)
-    if (m <= 64 * 2) GLL_REG(64, 2);
-    if (m <= 64 * 4) GLL_REG(64, 4);
-    if (m <= 64 * 8) GLL_REG(64, 8);
-    if (m <= 64 * 16) GLL_REG(64, 16);
-    if (m <= 256 * 8) GLL_REG(256, 8);
-    if (m <= 256 * 16) GLL_REG(256, 16);
-    if (m <= 1024 * 8) GLL_REG(1024, 8);
-#undef GLL_REG
+#define GLL_ELL(NT, R, S) \
+    return run_ell<NT, R, S, TB>(L, ws, b, out64, out32, rtol, max_iter, st_nonconv, st_iters, s)
+    if (m <= 64) GLL_ELL(64, 1, 16);
+    if (m <= 128) GLL_ELL(128, 1, 16);
+    if (m <= 256) GLL_ELL(256, 1, 16);
+    if (m <= 512) GLL_ELL(512, 1, 16);
+    if (m <= 1024) GLL_ELL(1024, 1, 16);
+    if (m <= 2048) GLL_ELL(1024, 2, 8);
+    if (m <= 4096) GLL_ELL(1024, 4, 6);
+#undef GLL_ELL
     const size_t vec_bytes = size_t(5) * m * sizeof(float);
     const bool vec_lds = 64 * 4 + vec_bytes <= kLdsLimit;
     const size_t lds = 64 * 4 + (vec_lds ? vec_bytes : 0);
