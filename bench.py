@@ -57,11 +57,8 @@ def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps):
     u = {
         "gram_d2_kernel": ("mfma", 2.0 * n * n * d),
         "knn_select_kernel": ("hbm", 4.0 * n * n + 8.0 * n * K),
-        "pair_flag_kernel": ("hbm", 8.0 * n * K + n * K),
-        "row_scan_kernel": ("hbm", 12.0 * n),
-        "fill_kernel": ("hbm", 8.0 * n * K + n * K + 8.0 * E),
-        "row_finalize_kernel": ("hbm", 8.0 * E + 4 * n + 4 * m * C + 12.0 * E),
-        "cg_luu_kernel": ("hbm", 0.5 * (iters_fwd + iters_bwd) * cg_iter),
+        "row_build_kernel": ("hbm", 16.0 * E + 8.0 * n * K + 4 * n + 4 * m * C),
+        "cg_kernel": ("hbm", 0.5 * (iters_fwd + iters_bwd) * cg_iter),
         "edge_coef_kernel": ("hbm", 16.0 * E + 8.0 * n * C),
         "grad_spmm_kernel": ("hbm", (12.0 * E + 8.0 * n * d) if auto_eps
                              else (8.0 * E + 8.0 * n * C + 8.0 * n * d)),
@@ -112,7 +109,6 @@ def main():
     Y = torch.from_numpy(one_hot(lab[: c["base"]])).to(dev)
     gbar = torch.from_numpy(seeded_gbar(c["batch"], 10, 1234 + rank)).to(dev)
     lap = GLL.LaplaceLearningSparseHard.apply
-    GLL.CHECK_STATUS = True
 
     def step():
         U = lap(X, Y, tau, eps, k)
@@ -171,7 +167,7 @@ def main():
         col = g["col"].cpu().numpy()
         rows = np.repeat(np.arange(c["n"]), np.diff(rp))
         nnz_uu = int(np.sum((rows >= c["base"]) & (col >= c["base"])))
-        GLL._poll_status(block=True)
+        GLL.check_status()
         iters = _cg_iters(X, Y, tau, eps, k, gbar)
         units = kernel_units(c, (int(rp[-1]), nnz_uu), iters[0], iters[1], isinstance(eps, str))
         bound, work = units[dominant]

@@ -33,40 +33,68 @@ DEFAULT_K = 25          # GLL.py:27
 DEFAULT_RTOL = 1e-6     # fp32 Jacobi-CG at 1e-6 matches SuperLU to <1e-5
 DEFAULT_MAX_ITER = 1000
 
-CHECK_STATUS = True     # asynchronous device-status -> Python warnings (no host sync)
+# Device status -> the reference's warnings, without a host sync on the hot path: every
+# call's kernels OR/max/add their status words into a sticky per-device sink (gll_problem.
+# status_sink); every FLUSH_EVERY calls the sink is copied to pinned memory and cleared on
+# the stream, and completed copies are turned into warnings at the next call.
+FLUSH_EVERY = 64
 _pending = collections.deque()
+_sinks = {}
+
+
+def _sink(dev: torch.device):
+    s = _sinks.get(dev.index)
+    if s is None:
+        s = _sinks[dev.index] = [torch.zeros(_lib.ST_NWORDS, dtype=torch.int32, device=dev), 0]
+    return s
+
+
+def _warn_from(st):
+    if st[_lib.ST_TINY_EPS]:
+        warnings.warn("Epsilon in KNN is very close to zero.", UserWarning)  # GLL.py:240-241
+    if st[_lib.ST_FWD_NONCONV]:
+        warnings.warn(f"GLL forward CG: {st[_lib.ST_FWD_NONCONV]} column solve(s) reached "
+                      f"max_iter ({st[_lib.ST_FWD_ITERS]} iterations)", RuntimeWarning)
+    if st[_lib.ST_BWD_NONCONV]:
+        warnings.warn(f"GLL adjoint CG: {st[_lib.ST_BWD_NONCONV]} column solve(s) reached "
+                      f"max_iter ({st[_lib.ST_BWD_ITERS]} iterations)", RuntimeWarning)
 
 
 def _poll_status(block: bool = False):
-    """Turn completed device status words into the reference's warnings."""
     while _pending:
-        ev, host, which = _pending[0]
+        ev, host = _pending[0]
         if not block and not ev.query():
             return
         ev.synchronize()
         _pending.popleft()
-        st = host.tolist()
-        if which == "fwd":
-            if st[_lib.ST_TINY_EPS]:
-                warnings.warn("Epsilon in KNN is very close to zero.", UserWarning)  # GLL.py:241
-            if st[_lib.ST_FWD_NONCONV]:
-                warnings.warn(f"GLL forward CG: {st[_lib.ST_FWD_NONCONV]} column(s) reached "
-                              f"max_iter ({st[_lib.ST_FWD_ITERS]} iters)", RuntimeWarning)
-        elif st[_lib.ST_BWD_NONCONV]:
-            warnings.warn(f"GLL adjoint CG: {st[_lib.ST_BWD_NONCONV]} column(s) reached "
-                          f"max_iter ({st[_lib.ST_BWD_ITERS]} iters)", RuntimeWarning)
+        _warn_from(host.tolist())
 
 
-def _queue_status(ws: torch.Tensor, which: str):
-    if not CHECK_STATUS:
-        return
+def _flush(dev: torch.device):
+    s = _sink(dev)
     host = torch.empty(_lib.ST_NWORDS, dtype=torch.int32, pin_memory=True)
-    host.copy_(ws[: 4 * _lib.ST_NWORDS].view(torch.int32), non_blocking=True)
+    host.copy_(s[0], non_blocking=True)
     ev = torch.cuda.Event()
     ev.record()
-    _pending.append((ev, host, which))
-    while len(_pending) > 64:
-        _poll_status(block=True)
+    s[0].zero_()
+    s[1] = 0
+    _pending.append((ev, host))
+
+
+def _after_call(dev: torch.device):
+    s = _sink(dev)
+    s[1] += 1
+    if s[1] >= FLUSH_EVERY:
+        _flush(dev)
+
+
+def check_status():
+    """Flush every device's status sink now and raise the pending warnings (syncs)."""
+    for idx in list(_sinks):
+        dev = torch.device("cuda", idx)
+        with torch.cuda.device(dev):
+            _flush(dev)
+    _poll_status(block=True)
 
 
 def _device_for(X: torch.Tensor) -> torch.device:
@@ -134,6 +162,7 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
             X32 = _features(X, dev)
             Y, ydt = _typed(label_matrix, dev)
             prob = make_problem(n, d, base, C, k, tau, epsilon)
+            prob.status_sink = _sink(dev)[0].data_ptr()
             nbytes = _lib.lib().gll_workspace_bytes(ct.byref(prob))
             if nbytes == 0:
                 raise ValueError(f"unsupported GLL problem n={n} d={d} base={base} C={C} k={k}")
@@ -142,7 +171,7 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
             _lib.check(_lib.lib().gll_forward(ct.byref(prob), X32.data_ptr(), Y.data_ptr(), ydt,
                                               ws.data_ptr(), U.data_ptr(), _stream(dev)),
                        "gll_forward")
-            _queue_status(ws, "fwd")
+            _after_call(dev)
         ctx.save_for_backward(X)
         ctx.prob, ctx.ws, ctx.dev = prob, ws, dev
         return U if X.is_cuda else U.cpu()
@@ -161,7 +190,6 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
                                                ctx.ws.data_ptr(), g.data_ptr(), gdt,
                                                gradX.data_ptr(), _stream(dev)),
                        "gll_backward")
-            _queue_status(ctx.ws, "bwd")
         if gradX.device != X.device or gradX.dtype != X.dtype:
             gradX = gradX.to(device=X.device, dtype=X.dtype)
         return gradX, None, None, None, None
@@ -195,16 +223,23 @@ def device_graph(X: torch.Tensor, k: int = DEFAULT_K, epsilon="auto"):
             esz = torch.empty(0, dtype=dtype).element_size()
             return ws[off: off + count * esz].view(dtype)
 
-        row_ptr = arr(view.row_ptr, n + 1, torch.int32)
+        # padded device rows (row_start, row_len) -> compact CSR
+        starts = arr(view.row_start, n, torch.int32).long()
+        lens = arr(view.row_len, n, torch.int32).long()
+        span = int((starts + lens).max().item())
+        row_ptr = torch.zeros(n + 1, dtype=torch.long, device=dev)
+        row_ptr[1:] = torch.cumsum(lens, 0)
         E = int(row_ptr[-1].item())
+        rows = torch.repeat_interleave(torch.arange(n, device=dev), lens)
+        src = starts[rows] + (torch.arange(E, device=dev) - row_ptr[rows])
         out = dict(
             knn_idx=arr(view.knn_idx, n * K, torch.int32).view(n, K),
             knn_d2=arr(view.knn_d2, n * K, torch.float32).view(n, K),
             eps=arr(view.eps, n, torch.float32),
-            row_ptr=row_ptr,
-            col=arr(view.col, E, torch.int32),
-            w=arr(view.w, E, torch.float32),
-            d2=arr(view.d2, E, torch.float32),
+            row_ptr=row_ptr.int(),
+            col=arr(view.col, span, torch.int32)[src],
+            w=arr(view.w, span, torch.float32)[src],
+            d2=arr(view.d2, span, torch.float32)[src],
             deg=arr(view.deg, n, torch.float32),
             workspace=ws,
         )

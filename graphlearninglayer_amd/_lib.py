@@ -16,8 +16,8 @@ GLL_OK = 0
 GLL_DT_F32, GLL_DT_F64, GLL_DT_I64 = 0, 1, 2
 ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
 ST_NWORDS = 16
-K_GRAM, K_SELECT, K_MUTUAL, K_SCAN, K_FILL, K_FINALIZE, K_CG, K_EDGE, K_GRAD = range(9)
-K_COUNT = 9
+K_GRAM, K_SELECT, K_FINALIZE, K_CG, K_EDGE, K_GRAD = range(6)
+K_COUNT = 6
 
 # every symbol include/gll.h declares (tests check the library exports all of them)
 EXPORTS = (
@@ -31,13 +31,14 @@ class Problem(ct.Structure):
     _fields_ = [
         ("n", ct.c_int32), ("d", ct.c_int32), ("base", ct.c_int32), ("C", ct.c_int32),
         ("K", ct.c_int32), ("max_iter", ct.c_int32), ("tau", ct.c_float), ("eps", ct.c_float),
-        ("rtol", ct.c_float), ("flags", ct.c_int32),
+        ("rtol", ct.c_float), ("flags", ct.c_int32), ("status_sink", ct.c_void_p),
     ]
 
 
 class View(ct.Structure):
     _fields_ = [(name, ct.c_void_p) for name in (
-        "knn_idx", "knn_d2", "eps", "row_ptr", "col", "w", "d2", "deg", "U32", "wadj", "status")]
+        "knn_idx", "knn_d2", "eps", "row_start", "row_len", "col", "w", "d2", "deg", "U32",
+        "wadj", "status")]
 
 
 _lock = threading.Lock()

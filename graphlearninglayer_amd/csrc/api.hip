@@ -57,9 +57,8 @@ void prof_end(int kid, hipStream_t s) {
 }
 
 static const char* kKernelNames[GLL_K_COUNT] = {
-    "gram_d2_kernel",   "knn_select_kernel", "pair_flag_kernel",
-    "row_scan_kernel",  "fill_kernel",       "row_finalize_kernel",
-    "cg_luu_kernel",    "edge_coef_kernel",  "grad_spmm_kernel"};
+    "gram_d2_kernel", "knn_select_kernel", "row_build_kernel",
+    "cg_kernel",      "edge_coef_kernel",  "grad_spmm_kernel"};
 
 static bool vec_ok(const float* X, int d) {
     return (d % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
@@ -79,19 +78,20 @@ static int check(const gll_problem* p) {
 
 static int hip_status(hipError_t e) { return e == hipSuccess ? GLL_OK : GLL_ERR_HIP; }
 
-static int build_graph(const gll_problem* p, const Layout& L, const float* X, void* ws,
-                       hipStream_t s) {
+// Status words the caller reads: the sticky sink when given, else the workspace block.
+static int32_t* public_status(const gll_problem* p, const Layout& L, void* ws) {
+    return p->status_sink ? p->status_sink : L.at<int32_t>(ws, L.status);
+}
+
+// kNN graph: gram (MFMA) -> select (+ reverse scatter) -> row build (+ weights, rhs)
+static int build_graph(const gll_problem* p, const Layout& L, const float* X, const void* Y,
+                       int y_dtype, void* ws, hipStream_t s) {
     const bool vec = vec_ok(X, p->d);
     const bool auto_eps = !(p->eps > 0.f);
-    int32_t* st = L.at<int32_t>(ws, L.status);
-    hipError_t e = launch_gram(X, L.n, L.d, L.at<float>(ws, L.D2), L.ldD, st, vec, s);
-    if (e != hipSuccess) return GLL_ERR_HIP;
-    e = launch_select(L.at<float>(ws, L.D2), L.ldD, X, L.n, L.d, L.K, p->eps, auto_eps,
-                      L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2),
-                      L.at<float>(ws, L.eps), L.at<int32_t>(ws, L.fwd_cnt),
-                      L.at<int32_t>(ws, L.rev_cnt), L.at<int32_t>(ws, L.fill_cnt), st, vec, s);
-    if (e != hipSuccess) return GLL_ERR_HIP;
-    return hip_status(launch_graph_build(L, ws, s));
+    if (launch_gram(L, ws, X, vec, s) != hipSuccess) return GLL_ERR_HIP;
+    if (launch_select(L, ws, X, p->eps, auto_eps, vec, public_status(p, L, ws), s) != hipSuccess)
+        return GLL_ERR_HIP;
+    return hip_status(launch_finalize(L, ws, Y, y_dtype, p->tau, s));
 }
 
 }  // namespace gll
@@ -111,11 +111,8 @@ int gll_graph(const gll_problem* p, const float* X, void* ws, void* stream) {
     if (!X || !ws) return GLL_ERR_INVALID_ARG;
     if (p->base != 0) return GLL_ERR_INVALID_ARG;  // graph only: no labeled block
     Layout L(*p);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    rc = build_graph(p, L, X, ws, s);
-    if (rc != GLL_OK) return rc;
-    // base = 0: every row is "unlabeled", rhs = 0 and no label read
-    return hip_status(launch_finalize(L, ws, nullptr, GLL_DT_F32, p->tau, s));
+    // base = 0: every row is "unlabeled", rhs = 0 and no label is read
+    return build_graph(p, L, X, nullptr, GLL_DT_F32, ws, static_cast<hipStream_t>(stream));
 }
 
 int gll_forward(const gll_problem* p, const float* X, const void* Y, int y_dtype, void* ws,
@@ -125,12 +122,11 @@ int gll_forward(const gll_problem* p, const float* X, const void* Y, int y_dtype
     if (!X || !ws || (p->base > 0 && !Y) || (p->n > p->base && !U)) return GLL_ERR_INVALID_ARG;
     Layout L(*p);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    rc = build_graph(p, L, X, ws, s);
+    rc = build_graph(p, L, X, Y, y_dtype, ws, s);
     if (rc != GLL_OK) return rc;
-    if (launch_finalize(L, ws, Y, y_dtype, p->tau, s) != hipSuccess) return GLL_ERR_HIP;
     const float rtol = p->rtol > 0.f ? p->rtol : 1e-6f;
     const int max_iter = p->max_iter > 0 ? p->max_iter : 1000;
-    int32_t* st = L.at<int32_t>(ws, L.status);
+    int32_t* st = public_status(p, L, ws);
     float* U32 = L.at<float>(ws, L.P) + size_t(L.base) * L.C;
     return hip_status(launch_cg_luu(L, ws, L.at<float>(ws, L.rhs), GLL_DT_F32, U, U32, rtol,
                                     max_iter, st + GLL_ST_FWD_NONCONV, st + GLL_ST_FWD_ITERS, s));
@@ -148,7 +144,7 @@ int gll_backward(const gll_problem* p, const float* X, const void* Y, int y_dtyp
     hipStream_t s = static_cast<hipStream_t>(stream);
     const float rtol = p->rtol > 0.f ? p->rtol : 1e-6f;
     const int max_iter = p->max_iter > 0 ? p->max_iter : 1000;
-    int32_t* st = L.at<int32_t>(ws, L.status);
+    int32_t* st = public_status(p, L, ws);
     float* wU = L.at<float>(ws, L.Wadj) + size_t(L.base) * L.C;
     // adjoint solve: Luu is symmetric, so Luu^-T gbar = Luu^-1 gbar (GLL.py:93)
     hipError_t e = launch_cg_luu(L, ws, gbar, g_dtype, nullptr, wU, rtol, max_iter,
@@ -166,7 +162,8 @@ int gll_workspace_view(const gll_problem* p, void* ws, gll_view* out) {
     out->knn_idx = L.at<int32_t>(ws, L.knn_idx);
     out->knn_d2 = L.at<float>(ws, L.knn_d2);
     out->eps = L.at<float>(ws, L.eps);
-    out->row_ptr = L.at<int32_t>(ws, L.row_ptr);
+    out->row_start = L.at<int32_t>(ws, L.row_start);
+    out->row_len = L.at<int32_t>(ws, L.row_len);
     out->col = L.at<int32_t>(ws, L.col);
     out->w = L.at<float>(ws, L.w);
     out->d2 = L.at<float>(ws, L.d2e);

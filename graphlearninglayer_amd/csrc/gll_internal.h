@@ -14,12 +14,22 @@ constexpr int kWave = 64;
 // ---------------------------------------------------------------------------------------
 // Workspace layout.  One block per forward/backward pair, carved into 256-B aligned arrays.
 // All sizes are functions of (n, d, base, C, K) only, so forward and backward agree.
+//
+// Graph storage ("padded rows"): row i of the symmetric kNN graph holds row_len[i] entries
+// (col, w, d2) starting at row_start[i], sorted by column.  Ordinary rows sit in a fixed slot
+// i * Wcap (Wcap = (K-1) + RCAP); rows whose reverse list overflowed (hubs) get their
+// storage from a bump region behind the slots.  No prefix sum over rows is ever needed.
 // ---------------------------------------------------------------------------------------
+constexpr int kStOvfCount = 8;   // internal status words: overflow-list length
+constexpr int kStBump = 9;       //                        bump-region cursor
+
 struct Layout {
     int n, d, base, m, C, K;
     int ldD;          // leading dimension of the n x n squared-distance matrix
-    int64_t Emax;     // upper bound on directed edges: 2 n (K-1)
-    size_t status, D2, knn_idx, knn_d2, flag, eps, fwd_cnt, rev_cnt, fill_cnt, row_ptr;
+    int RCAP;         // reverse-list capacity per row
+    int Wcap;         // slot width of a row
+    int64_t Etot;     // entry capacity: n Wcap slots + 2 n (K-1) bump region
+    size_t status, D2, knn_idx, knn_d2, eps, rev_cnt, rev_idx, rev_d2, ovf, row_start, row_len;
     size_t tmp_col, tmp_d2, col, w, d2e, deg, ucnt, diag, rhs, P, Wadj, S, b, cgv, total;
 
     explicit Layout(const gll_problem& p) {
@@ -27,7 +37,9 @@ struct Layout {
         K = p.K < p.n ? p.K : p.n;
         m = n - base;
         ldD = (n + 3) & ~3;
-        Emax = 2LL * n * (K - 1);
+        RCAP = 4 * (K - 1) + 8;
+        Wcap = (K - 1) + RCAP;
+        Etot = int64_t(n) * Wcap + 2LL * n * (K - 1);
         size_t off = 0;
         auto take = [&](size_t bytes) {
             size_t at = off;
@@ -38,24 +50,25 @@ struct Layout {
         D2 = take(size_t(n) * ldD * 4);
         knn_idx = take(size_t(n) * K * 4);
         knn_d2 = take(size_t(n) * K * 4);
-        flag = take(size_t(n) * K);
         eps = take(size_t(n) * 4);
-        fwd_cnt = take(size_t(n) * 4);
         rev_cnt = take(size_t(n) * 4);
-        fill_cnt = take(size_t(n) * 4);
-        row_ptr = take(size_t(n + 1) * 4);
-        tmp_col = take(size_t(Emax) * 4);
-        tmp_d2 = take(size_t(Emax) * 4);
-        col = take(size_t(Emax) * 4);
-        w = take(size_t(Emax) * 4);
-        d2e = take(size_t(Emax) * 4);
+        rev_idx = take(size_t(n) * RCAP * 4);
+        rev_d2 = take(size_t(n) * RCAP * 4);
+        ovf = take(size_t(n) * (K - 1) * 12);   // (row, col, d2) triples past RCAP
+        row_start = take(size_t(n) * 4);
+        row_len = take(size_t(n) * 4);
+        tmp_col = take(size_t(Etot) * 4);       // staging of rows too long for LDS
+        tmp_d2 = take(size_t(Etot) * 4);
+        col = take(size_t(Etot) * 4);
+        w = take(size_t(Etot) * 4);
+        d2e = take(size_t(Etot) * 4);
         deg = take(size_t(n) * 4);
         ucnt = take(size_t(m) * 4);        // U-block entries per unlabeled row
         diag = take(size_t(m) * 4);
         rhs = take(size_t(m) * C * 4);
         P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)
         Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
-        S = take(size_t(Emax) * 4);        // per-edge coefficient (auto eps only)
+        S = take(size_t(Etot) * 4);        // per-edge coefficient (auto eps only)
         b = take(size_t(n) * 4);           // auto-eps b_i (GLL.py:126)
         cgv = take(size_t(5) * m * C * 4); // CG vectors when they do not fit in LDS
         total = off;
@@ -117,6 +130,40 @@ __device__ __forceinline__ void wave_sum2_dpp(float& a, float& b) {
     b = readlane_f(b, 63);
 }
 
+// Wave64 minimum of a 64-bit key through DPP; result broadcast to every lane.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint64_t dpp_min_u64(uint64_t k) {
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0xFFFFFFFFu, uint32_t(k), CTRL, ROW_MASK, 0xf,
+                                                    false);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0xFFFFFFFFu, uint32_t(k >> 32), CTRL,
+                                                    ROW_MASK, 0xf, false);
+    const uint64_t o = (uint64_t(hi) << 32) | lo;
+    return o < k ? o : k;
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t k) {
+    k = dpp_min_u64<0xB1, 0xf>(k);
+    k = dpp_min_u64<0x4E, 0xf>(k);
+    k = dpp_min_u64<0x141, 0xf>(k);
+    k = dpp_min_u64<0x140, 0xf>(k);
+    k = dpp_min_u64<0x142, 0xa>(k);
+    k = dpp_min_u64<0x143, 0xc>(k);
+    const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(k), 63);
+    const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(k >> 32), 63);
+    return (uint64_t(hi) << 32) | lo;
+}
+// Sum over each aligned group of 8 lanes (result in all 8 lanes of the group).
+__device__ __forceinline__ float group8_sum(float v) {
+    v = dpp_add<0xB1, 0xf>(v);
+    v = dpp_add<0x4E, 0xf>(v);
+    v = dpp_add<0x141, 0xf>(v);
+    return v;
+}
+// Number of set bits of `mask` below this lane (wave-level compaction).
+__device__ __forceinline__ int lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi(uint32_t(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo(uint32_t(mask), 0));
+}
+
 template <typename T>
 __device__ __forceinline__ float to_f32(T v) { return static_cast<float>(v); }
 
@@ -143,13 +190,9 @@ __device__ __forceinline__ f32x4 load4(const float* __restrict__ p, int k, int l
 void prof_begin(int kid, hipStream_t s);
 void prof_end(int kid, hipStream_t s);
 
-hipError_t launch_gram(const float* X, int n, int d, float* D2, int ldD, int32_t* status,
-                       bool vec, hipStream_t s);
-hipError_t launch_select(const float* D2, int ldD, const float* X, int n, int d, int K,
-                         float eps_fixed, bool auto_eps, int32_t* knn_idx, float* knn_d2,
-                         float* eps, int32_t* fwd_cnt, int32_t* rev_cnt, int32_t* fill_cnt,
-                         int32_t* status, bool vec, hipStream_t s);
-hipError_t launch_graph_build(const Layout& L, void* ws, hipStream_t s);
+hipError_t launch_gram(const Layout& L, void* ws, const float* X, bool vec, hipStream_t s);
+hipError_t launch_select(const Layout& L, void* ws, const float* X, float eps_fixed,
+                         bool auto_eps, bool vec, int32_t* status_pub, hipStream_t s);
 hipError_t launch_finalize(const Layout& L, void* ws, const void* Y, int y_dtype, float tau,
                            hipStream_t s);
 hipError_t launch_cg_luu(const Layout& L, void* ws, const void* b, int b_dtype, double* out64,

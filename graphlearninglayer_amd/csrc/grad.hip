@@ -18,7 +18,8 @@ namespace gll {
 
 struct EdgeArgs {
     int n, base, C, K, d;
-    const int32_t* row_ptr;
+    const int32_t* row_start;
+    const int32_t* row_len;
     const int32_t* col;
     const float* w;       // W_ij
     const float* d2;      // d_ij^2
@@ -49,7 +50,7 @@ __global__ __launch_bounds__(256) void edge_coef_kernel(EdgeArgs a) {
     const int lane = lane_id();
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
-    const int beg = a.row_ptr[i], end = a.row_ptr[i + 1];
+    const int beg = a.row_start[i], end = beg + a.row_len[i];
     const float ei = a.eps[i];
     float bpart = 0.f;
     for (int e = beg + lane; e < end; e += kWave) {
@@ -70,7 +71,7 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
     const int d = a.d;
-    const int beg = a.row_ptr[i], end = a.row_ptr[i + 1];
+    const int beg = a.row_start[i], end = beg + a.row_len[i];
     const float ei = a.eps[i];
     int kth_i = 0;
     float b_i = 0.f;
@@ -153,7 +154,8 @@ hipError_t launch_backward_grad(const Layout& L, void* ws, const float* X, bool 
     a.C = L.C;
     a.K = L.K;
     a.d = L.d;
-    a.row_ptr = L.at<int32_t>(ws, L.row_ptr);
+    a.row_start = L.at<int32_t>(ws, L.row_start);
+    a.row_len = L.at<int32_t>(ws, L.row_len);
     a.col = L.at<int32_t>(ws, L.col);
     a.w = L.at<float>(ws, L.w);
     a.d2 = L.at<float>(ws, L.d2e);

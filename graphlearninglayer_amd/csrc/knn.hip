@@ -5,11 +5,18 @@
 //                       64x64 output tile per 256-thread workgroup, one 32x32 tile per wave,
 //                       operands streamed straight to VGPRs (the f32 MFMA needs one VGPR per
 //                       operand per lane), row norms accumulated from the same loads.
-//  K1b knn_select_kernel one wave per row: per-lane sorted candidate lists over the D2 row,
-//                       a 64-lane merge to kc = K-1+margin candidates, exact re-ranking with
-//                       d^2 = sum_k (x_ik - x_jk)^2 (bitwise symmetric in i,j), then the K-1
-//                       nearest with ties broken by index.  Self is forced to rank 0 with
-//                       distance 0 (the stand-in contract of SURVEY.md §8c).
+//  K1b knn_select_kernel one wave per row:
+//                       1. per-lane sorted candidate lists over the D2 row (16-B loads);
+//                       2. a 64-lane merge to kc = K-1+margin candidates, one DPP arg-min of
+//                          the packed (d2, index) key per round;
+//                       3. exact re-ranking with d^2 = sum_k (x_ik - x_jk)^2, eight candidates
+//                          at a time (8-lane groups, DPP group sums) -- bitwise symmetric in
+//                          (i, j) because both orders run the same lane mapping;
+//                       4. the K-1 nearest by (exact d^2, index); self forced to rank 0 with
+//                          distance 0 (the stand-in contract of SURVEY.md §8c);
+//                       5. every valid pair (i -> j) is pushed onto j's reverse list (or the
+//                          overflow list), which is how the symmetric union of GLL.py:197 is
+//                          built without an n x n structure or a prefix sum.
 #include <limits.h>
 
 #include "gll_internal.h"
@@ -22,14 +29,20 @@ namespace gll {
 template <bool VEC>
 __global__ __launch_bounds__(256) void gram_d2_kernel(const float* __restrict__ X, int n, int d,
                                                       float* __restrict__ D2, int ld,
-                                                      int32_t* __restrict__ status) {
+                                                      int32_t* __restrict__ status,
+                                                      int32_t* __restrict__ rev_cnt) {
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     const int r = lane & 31;   // A row / B column owned by this lane
     const int h = lane >> 5;   // k half: lane holds k = k0 + 4h + t, t = 0..3
     const int row0 = blockIdx.y * 64 + (wave >> 1) * 32;
     const int col0 = blockIdx.x * 64 + (wave & 1) * 32;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < GLL_ST_NWORDS) status[threadIdx.x] = 0;
+    // per-call reset of the counters the select kernel accumulates into
+    {
+        const int g = (blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
+        if (g < GLL_ST_NWORDS) status[g] = 0;
+        for (int q = g; q < n; q += gridDim.x * gridDim.y * 256) rev_cnt[q] = 0;
+    }
 
     const float* pa = X + size_t(min(row0 + r, n - 1)) * d + 4 * h;
     const float* pb = X + size_t(min(col0 + r, n - 1)) * d + 4 * h;
@@ -84,92 +97,76 @@ __global__ __launch_bounds__(256) void gram_d2_kernel(const float* __restrict__ 
 }
 
 // --------------------------------------------------------------------------------------
-// K1b: per-row selection + exact re-rank
+// K1b: per-row selection + exact re-rank + reverse scatter
 // --------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t pack_key(float d2, int j) {
+    // d2 >= 0 after the clamp, so its IEEE bits order like the value; index breaks ties
+    return (uint64_t(__float_as_uint(d2 > 0.f ? d2 : 0.f)) << 32) | uint32_t(j);
+}
+
 template <int KC>
-__device__ __forceinline__ void list_insert(float (&key)[KC], int (&idx)[KC], float v, int j) {
-    // precondition: v < key[KC-1]; keeps ascending order, equal keys keep scan order
+__device__ __forceinline__ void list_insert(uint64_t (&key)[KC], uint64_t v) {
+    // precondition: v < key[KC-1]; ascending order kept (keys are unique)
 #pragma unroll
     for (int t = KC - 1; t > 0; --t) {
-        const bool shift = key[t - 1] > v;
-        const bool here = key[t] > v;
-        key[t] = shift ? key[t - 1] : (here ? v : key[t]);
-        idx[t] = shift ? idx[t - 1] : (here ? j : idx[t]);
+        const uint64_t prev = key[t - 1];
+        key[t] = prev > v ? prev : (key[t] > v ? v : key[t]);
     }
-    const bool here0 = key[0] > v;
-    key[0] = here0 ? v : key[0];
-    idx[0] = here0 ? j : idx[0];
+    key[0] = key[0] > v ? v : key[0];
 }
 
 template <int KC>
-__device__ __forceinline__ void list_pop(float (&key)[KC], int (&idx)[KC], bool pop) {
+__device__ __forceinline__ void list_pop(uint64_t (&key)[KC], bool pop) {
 #pragma unroll
-    for (int t = 0; t < KC - 1; ++t) {
-        key[t] = pop ? key[t + 1] : key[t];
-        idx[t] = pop ? idx[t + 1] : idx[t];
-    }
-    key[KC - 1] = pop ? __builtin_inff() : key[KC - 1];
-    idx[KC - 1] = pop ? INT_MAX : idx[KC - 1];
-}
-
-__device__ __forceinline__ bool lex_less(float ka, int ia, float kb, int ib) {
-    return ka < kb || (ka == kb && ia < ib);
+    for (int t = 0; t < KC - 1; ++t) key[t] = pop ? key[t + 1] : key[t];
+    key[KC - 1] = pop ? ~0ull : key[KC - 1];
 }
 
 template <int KC, bool VEC>
 __global__ __launch_bounds__(256) void knn_select_kernel(
     const float* __restrict__ D2, int ld, const float* __restrict__ X, int n, int d, int K,
-    int kc, float eps_fixed, int auto_eps, int32_t* __restrict__ knn_idx,
-    float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ fwd_cnt,
-    int32_t* __restrict__ rev_cnt, int32_t* __restrict__ fill_cnt, int32_t* __restrict__ status) {
+    int kc, float eps_fixed, int auto_eps, int RCAP, int32_t* __restrict__ knn_idx,
+    float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ rev_cnt,
+    int32_t* __restrict__ rev_idx, float* __restrict__ rev_d2, int32_t* __restrict__ ovf,
+    int32_t* __restrict__ status, int32_t* __restrict__ status_pub) {
     const int lane = lane_id();
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;  // whole wave
 
-    float key[KC];
-    int idx[KC];
+    // 1) per-lane scan of the row
+    uint64_t key[KC];
 #pragma unroll
-    for (int t = 0; t < KC; ++t) {
-        key[t] = __builtin_inff();
-        idx[t] = INT_MAX;
-    }
-    // 1) per-lane scan of the row (16-B loads: lane covers 4 consecutive columns)
+    for (int t = 0; t < KC; ++t) key[t] = ~0ull;
     const float* row = D2 + size_t(i) * ld;
     for (int j0 = 4 * lane; j0 < n; j0 += 4 * kWave) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(row + j0);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int j = j0 + t;
-            const float x = v[t];
-            if (j < n && j != i && x < key[KC - 1]) list_insert<KC>(key, idx, x, j);
-        }
-    }
-    // 2) merge: round t hands the t-th smallest (key, idx) to lane t
-    int ci = INT_MAX;
-    for (int t = 0; t < kc; ++t) {
-        float bk = key[0];
-        int bi = idx[0];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const float ok = __shfl_xor(bk, off);
-            const int oi = __shfl_xor(bi, off);
-            if (lex_less(ok, oi, bk, bi)) {
-                bk = ok;
-                bi = oi;
+            if (j < n && j != i && v[t] == v[t]) {   // NaN rows never enter
+                const uint64_t kv = pack_key(v[t], j);
+                if (kv < key[KC - 1]) list_insert<KC>(key, kv);
             }
         }
-        if (lane == t) ci = bi;
-        list_pop<KC>(key, idx, bi != INT_MAX && idx[0] == bi);
     }
-    // 3) exact squared distances of the candidates, lanes across the feature dimension
+    // 2) merge: round t hands the t-th smallest key to lane t
+    uint64_t mine = ~0ull;
+    for (int t = 0; t < kc; ++t) {
+        const uint64_t best = wave_min_u64(key[0]);
+        if (lane == t) mine = best;
+        list_pop<KC>(key, best != ~0ull && key[0] == best);
+    }
+    const int ci = mine == ~0ull ? -1 : int(uint32_t(mine));
+    // 3) exact squared distances, 8 candidates per pass (8 lanes each, across d)
+    const int grp = lane >> 3, sub = lane & 7;
     const float* xi = X + size_t(i) * d;
     float ce = __builtin_inff();
-    for (int t = 0; t < kc; ++t) {
-        const int j = readlane_i(ci, t);
-        if (j == INT_MAX) continue;  // wave-uniform
-        const float* xj = X + size_t(j) * d;
+    for (int p0 = 0; p0 < kc; p0 += 8) {
+        const int j = __shfl(ci, p0 + grp < kc ? p0 + grp : 0);
+        const bool live = p0 + grp < kc && j >= 0;
+        const float* xj = X + size_t(live ? j : i) * d;
         float part = 0.f;
-        for (int k = 4 * lane; k < d; k += 4 * kWave) {
+        for (int k = 4 * sub; k < d; k += 32) {
             const f32x4 a = load4<VEC>(xi, k, d);
             const f32x4 bb = load4<VEC>(xj, k, d);
             const f32x4 df = a - bb;
@@ -178,17 +175,24 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
             part += df.z * df.z;
             part += df.w * df.w;
         }
-        part = wave_sum(part);
-        if (lane == t) ce = part;
+        part = group8_sum(part);
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            const float v = readlane_f(part, 8 * g);
+            if (lane == p0 + g) ce = v;
+        }
     }
+    if (ci < 0) ce = __builtin_inff();
     // 4) rank the candidates by (exact d^2, index); keep the K-1 nearest
+    const uint64_t myk = ci < 0 ? ~0ull : pack_key(ce, ci);
     int rank = 0;
     for (int u = 0; u < kc; ++u) {
-        const float eu = __shfl(ce, u);
-        const int iu = __shfl(ci, u);
-        rank += (iu != INT_MAX && lex_less(eu, iu, ce, ci)) ? 1 : 0;
+        const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(myk), u);
+        const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(myk >> 32), u);
+        const uint64_t ku = (uint64_t(hi) << 32) | lo;
+        rank += ku < myk ? 1 : 0;
     }
-    const bool keep = lane < kc && ci != INT_MAX && rank < K - 1;
+    const bool keep = lane < kc && ci >= 0 && rank < K - 1;
     int32_t* oi = knn_idx + size_t(i) * K;
     float* od = knn_d2 + size_t(i) * K;
     if (lane == 0) {
@@ -199,43 +203,53 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
         oi[1 + rank] = ci;
         od[1 + rank] = ce;
     }
-    // rows with fewer valid candidates (non-finite input) fall back to self, distance 0,
+    // rows with fewer valid candidates (non-finite input) fall back to self at distance 0,
     // i.e. dropped edges (sparse.find drops zeros, GLL.py:198)
-    const int nkeep = wave_sum_i(keep ? 1 : 0);
+    const int nkeep = __popcll(__ballot(keep));
     if (lane >= nkeep && lane < K - 1) {
         oi[1 + lane] = i;
         od[1 + lane] = 0.f;
     }
-    const int nfwd = wave_sum_i((keep && ce > 0.f) ? 1 : 0);
     float ei = eps_fixed;
     if (auto_eps) {
         // eps_i = d(i, knn_ind[i, K-1])  (GLL.py:205)
-        float e = (keep && rank == K - 2) ? sqrtf(ce) : 0.f;
-        ei = wave_sum(e);
+        const float e = (keep && rank == K - 2) ? sqrtf(ce) : 0.f;
+        ei = wave_sum_dpp(e);
     }
     if (lane == 0) {
-        fwd_cnt[i] = nfwd;
-        rev_cnt[i] = 0;
-        fill_cnt[i] = 0;
         eps[i] = ei;
-        if (!(ei >= 1e-10f)) atomicOr(&status[GLL_ST_TINY_EPS], 1);  // GLL.py:240-241
+        if (!(ei >= 1e-10f)) atomicOr(&status_pub[GLL_ST_TINY_EPS], 1);  // GLL.py:240-241
+    }
+    // 5) reverse entry (ci, i) for every valid pair; zero distances never enter the graph
+    if (keep && ce > 0.f) {
+        const int pos = atomicAdd(&rev_cnt[ci], 1);
+        if (pos < RCAP) {
+            rev_idx[size_t(ci) * RCAP + pos] = i;
+            rev_d2[size_t(ci) * RCAP + pos] = ce;
+        } else {
+            const int q = atomicAdd(&status[kStOvfCount], 1);
+            ovf[3 * q + 0] = ci;
+            ovf[3 * q + 1] = i;
+            ovf[3 * q + 2] = __float_as_int(ce);
+        }
     }
 }
 
-hipError_t launch_gram(const float* X, int n, int d, float* D2, int ldD, int32_t* status,
-                       bool vec, hipStream_t s) {
-    dim3 grid((n + 63) / 64, (n + 63) / 64);
+hipError_t launch_gram(const Layout& L, void* ws, const float* X, bool vec, hipStream_t s) {
+    dim3 grid((L.n + 63) / 64, (L.n + 63) / 64);
+    float* D2 = L.at<float>(ws, L.D2);
+    int32_t* st = L.at<int32_t>(ws, L.status);
+    int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
     prof_begin(GLL_K_GRAM, s);
-    if (vec) gram_d2_kernel<true><<<grid, 256, 0, s>>>(X, n, d, D2, ldD, status);
-    else gram_d2_kernel<false><<<grid, 256, 0, s>>>(X, n, d, D2, ldD, status);
+    if (vec) gram_d2_kernel<true><<<grid, 256, 0, s>>>(X, L.n, L.d, D2, L.ldD, st, rc);
+    else gram_d2_kernel<false><<<grid, 256, 0, s>>>(X, L.n, L.d, D2, L.ldD, st, rc);
     prof_end(GLL_K_GRAM, s);
     return hipGetLastError();
 }
 
-hipError_t launch_select(const float* D2, int ldD, const float* X, int n, int d, int K,
-                         float eps_fixed, bool auto_eps, int32_t* knn_idx, float* knn_d2,
-                         float* eps, int32_t* fwd_cnt, int32_t* rev_cnt, int32_t* fill_cnt,
-                         int32_t* status, bool vec, hipStream_t s) {
+hipError_t launch_select(const Layout& L, void* ws, const float* X, float eps_fixed,
+                         bool auto_eps, bool vec, int32_t* status_pub, hipStream_t s) {
+    const int n = L.n, K = L.K;
     // candidate list capacity: smallest of {16, 32, 64} leaving a re-rank margin >= 4
     const int need = K - 1 + 4;
     const int KC = need <= 16 ? 16 : (need <= 32 ? 32 : 64);
@@ -247,9 +261,11 @@ hipError_t launch_select(const float* D2, int ldD, const float* X, int n, int d,
     dim3 grid((n + 3) / 4);
     prof_begin(GLL_K_SELECT, s);
 #define GLL_SEL(KCV, V)                                                                        \
-    knn_select_kernel<KCV, V><<<grid, 256, 0, s>>>(D2, ldD, X, n, d, K, kc, eps_fixed,         \
-                                                   auto_eps ? 1 : 0, knn_idx, knn_d2, eps,     \
-                                                   fwd_cnt, rev_cnt, fill_cnt, status)
+    knn_select_kernel<KCV, V><<<grid, 256, 0, s>>>(                                            \
+        L.at<float>(ws, L.D2), L.ldD, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0, L.RCAP,    \
+        L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \
+        L.at<int32_t>(ws, L.rev_cnt), L.at<int32_t>(ws, L.rev_idx), L.at<float>(ws, L.rev_d2), \
+        L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub)
     if (KC == 16) { if (vec) GLL_SEL(16, true); else GLL_SEL(16, false); }
     else if (KC == 32) { if (vec) GLL_SEL(32, true); else GLL_SEL(32, false); }
     else { if (vec) GLL_SEL(64, true); else GLL_SEL(64, false); }

@@ -1,0 +1,264 @@
+// rows.hip -- symmetric kNN graph rows + weights, degree and Laplace right-hand side.
+//
+// Replaces the scipy COO/CSR work of knn_sym_dist (/root/reference/GLL.py:192-238:
+// coo->csr, symmetric max, sparse.find, W values) and csgraph.laplacian + the Luu/Lul
+// split (GLL.py:29,37-38,48).  One wave per graph row i (K3 row_build_kernel):
+//   * forward entries: i's own kNN list (valid = d > 0; sparse.find drops zeros, GLL.py:198);
+//   * reverse entries: every l that listed i (pushed by knn_select_kernel onto i's reverse
+//     list, spilling to the overflow list past RCAP), minus those already in i's own list:
+//     the union pattern of GLL.py:197 (distances are bitwise symmetric, so max = either);
+//   * the row is staged in LDS (global scratch for hub rows), rank-sorted by column --
+//     deterministic whatever order the atomics produced -- and written to its slot
+//     (row_start, row_len; hub rows take a bump-allocated range);
+//   * W_ij = exp(-4 d_ij^2 / (eps_i eps_j)) (GLL.py:216/233), degree, and for unlabeled rows
+//     the Luu diagonal deg + tau, the U-block length, and rhs = W_ul Y (= -Lul Y, GLL.py:53);
+//     labeled rows write P = Y and w = 0 for the backward (GLL.py:104,109).
+#include "gll_internal.h"
+
+namespace gll {
+
+constexpr int kStage = 256;      // per-wave LDS staging capacity (entries)
+constexpr int kMaxCPerLane = 4;  // classes per lane in the rhs accumulation (C <= 256)
+
+struct RowArgs {
+    int n, base, C, K, RCAP, Wcap;
+    int64_t bump_base;
+    float tau;
+    const int32_t* knn_idx;
+    const float* knn_d2;
+    const int32_t* rev_cnt;
+    const int32_t* rev_idx;
+    const float* rev_d2;
+    const int32_t* ovf;
+    int32_t* status;
+    const float* eps;
+    int32_t* tmp_col;
+    float* tmp_d2;
+    int32_t* row_start;
+    int32_t* row_len;
+    int32_t* col;
+    float* w;
+    float* d2e;
+    float* deg;
+    int32_t* ucnt;
+    float* diag;
+    float* rhs;
+    float* P;
+    float* Wadj;
+};
+
+template <typename TY>
+__device__ __forceinline__ float yval(const TY* Y, int j, int C, int c) {
+    return to_f32(Y[size_t(j) * C + c]);
+}
+
+// Build row i.  LDS: staging and sorted copies live in the wave's LDS slices; otherwise the
+// staging is tmp_col/tmp_d2 and the sorted copy is the output itself (agent fences order them).
+template <bool LDS, typename TY>
+__device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict__ Y, int i,
+                                          int start, int fi, float fd, bool fval,
+                                          uint64_t fmask, int nf, int rc, int* s_col,
+                                          float* s_d2, int* t_col, float* t_d2, float* t_w) {
+    const int lane = lane_id();
+    int* scol = LDS ? s_col : a.tmp_col + start;
+    float* sd2 = LDS ? s_d2 : a.tmp_d2 + start;
+    int* ocol = LDS ? t_col : a.col + start;
+    float* od2 = LDS ? t_d2 : a.d2e + start;
+    float* ow = LDS ? t_w : a.w + start;
+    const int Km1 = a.K - 1;
+    const int fself = fval ? fi : -2;
+    // forward entries
+    if (fval) {
+        const int p = lanes_below(fmask);
+        scol[p] = fi;
+        sd2[p] = fd;
+    }
+    int L = nf;
+    // reverse entries, deduplicated against the forward list (mutual pairs)
+    const int nr = min(rc, a.RCAP);
+    for (int r0 = 0; r0 < nr; r0 += kWave) {
+        const int r = r0 + lane;
+        const bool live = r < nr;
+        const int ri = live ? a.rev_idx[size_t(i) * a.RCAP + r] : -1;
+        const float rd = live ? a.rev_d2[size_t(i) * a.RCAP + r] : 0.f;
+        bool dup = false;
+        for (int t = 0; t < Km1; ++t) dup |= (ri == readlane_i(fself, t));
+        const bool keep = live && !dup;
+        const uint64_t mk = __ballot(keep);
+        if (keep) {
+            const int p = L + lanes_below(mk);
+            scol[p] = ri;
+            sd2[p] = rd;
+        }
+        L += __popcll(mk);
+    }
+    if (rc > a.RCAP) {  // hub row: the remaining reverse entries sit in the overflow list
+        const int novf = __hip_atomic_load(&a.status[kStOvfCount], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        for (int q0 = 0; q0 < novf; q0 += kWave) {
+            const int q = q0 + lane;
+            const bool live = q < novf;
+            const int oj = live ? a.ovf[3 * q] : -1;
+            const int oi = live ? a.ovf[3 * q + 1] : -1;
+            const float od = live ? __int_as_float(a.ovf[3 * q + 2]) : 0.f;
+            bool dup = false;
+            for (int t = 0; t < Km1; ++t) dup |= (oi == readlane_i(fself, t));
+            const bool keep = live && oj == i && !dup;
+            const uint64_t mk = __ballot(keep);
+            if (keep) {
+                const int p = L + lanes_below(mk);
+                scol[p] = oi;
+                sd2[p] = od;
+            }
+            L += __popcll(mk);
+        }
+    }
+    if constexpr (!LDS) __threadfence();
+    // rank sort by column (columns are unique within a row)
+    for (int e = lane; e < L; e += kWave) {
+        const int c = scol[e];
+        int rank = 0;
+        for (int u = 0; u < L; ++u) rank += scol[u] < c ? 1 : 0;
+        ocol[rank] = c;
+        od2[rank] = sd2[e];
+    }
+    if constexpr (!LDS) __threadfence();
+    // sorted pass: weights, degree, labeled-prefix length
+    const float ei = a.eps[i];
+    float dsum = 0.f;
+    int nlab = 0;
+    for (int e = lane; e < L; e += kWave) {
+        const int c = ocol[e];
+        const float dd = od2[e];
+        const float we = expf(-4.f * dd / (ei * a.eps[c]));   // GLL.py:216/233
+        ow[e] = we;
+        if constexpr (LDS) {
+            a.col[start + e] = c;
+            a.d2e[start + e] = dd;
+            a.w[start + e] = we;
+        }
+        dsum += we;
+        nlab += c < a.base ? 1 : 0;
+    }
+    if constexpr (!LDS) __threadfence();
+    dsum = wave_sum_dpp(dsum);
+    nlab = wave_sum_i(nlab);
+    // rhs_i = sum_{j < base} W_ij Y_j over the sorted labeled prefix, lanes over classes
+    float racc[kMaxCPerLane];
+#pragma unroll
+    for (int q = 0; q < kMaxCPerLane; ++q) racc[q] = 0.f;
+    if (i >= a.base) {
+        for (int e = 0; e < nlab; ++e) {
+            const int j = ocol[e];
+            const float we = ow[e];
+#pragma unroll
+            for (int q = 0; q < kMaxCPerLane; ++q) {
+                const int c = lane + q * kWave;
+                if (c < a.C) racc[q] += we * yval(Y, j, a.C, c);
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < kMaxCPerLane; ++q) {
+        const int c = lane + q * kWave;
+        if (c < a.C) {
+            if (i >= a.base) {
+                a.rhs[size_t(i - a.base) * a.C + c] = racc[q];
+            } else {
+                a.P[size_t(i) * a.C + c] = yval(Y, i, a.C, c);
+                a.Wadj[size_t(i) * a.C + c] = 0.f;
+            }
+        }
+    }
+    if (lane == 0) {
+        a.row_start[i] = start;
+        a.row_len[i] = L;
+        a.deg[i] = dsum;
+        if (i >= a.base) {
+            a.diag[i - a.base] = dsum + a.tau;   // Luu + tau I (GLL.py:48)
+            a.ucnt[i - a.base] = L - nlab;       // the U block is the row's sorted suffix
+        }
+    }
+}
+
+template <typename TY>
+__global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __restrict__ Y) {
+    __shared__ int s_col[4][kStage];
+    __shared__ float s_d2[4][kStage];
+    __shared__ int t_col[4][kStage];
+    __shared__ float t_d2[4][kStage];
+    __shared__ float t_w[4][kStage];
+    const int lane = lane_id();
+    const int wv = threadIdx.x >> 6;
+    const int i = blockIdx.x * 4 + wv;
+    if (i >= a.n) return;
+    const int Km1 = a.K - 1;
+    int fi = -1;
+    float fd = 0.f;
+    if (lane < Km1) {
+        fi = a.knn_idx[size_t(i) * a.K + 1 + lane];
+        fd = a.knn_d2[size_t(i) * a.K + 1 + lane];
+    }
+    const bool fval = lane < Km1 && fd > 0.f && fi != i && fi >= 0 && fi < a.n;
+    const uint64_t fmask = __ballot(fval);
+    const int nf = __popcll(fmask);
+    const int rc = a.rev_cnt[i];
+    const int lbound = nf + rc;
+    int start = i * a.Wcap;
+    if (lbound > a.Wcap) {
+        int s0 = 0;
+        if (lane == 0) s0 = int(a.bump_base) + atomicAdd(&a.status[kStBump], lbound);
+        start = readlane_i(s0, 0);
+    }
+    if (lbound <= kStage)
+        build_row<true, TY>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, s_col[wv], s_d2[wv],
+                            t_col[wv], t_d2[wv], t_w[wv]);
+    else
+        build_row<false, TY>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, nullptr, nullptr,
+                             nullptr, nullptr, nullptr);
+}
+
+hipError_t launch_finalize(const Layout& L, void* ws, const void* Y, int y_dtype, float tau,
+                           hipStream_t s) {
+    if (L.C > kMaxCPerLane * kWave) return hipErrorInvalidValue;
+    RowArgs a;
+    a.n = L.n;
+    a.base = L.base;
+    a.C = L.C;
+    a.K = L.K;
+    a.RCAP = L.RCAP;
+    a.Wcap = L.Wcap;
+    a.bump_base = int64_t(L.n) * L.Wcap;
+    a.tau = tau;
+    a.knn_idx = L.at<int32_t>(ws, L.knn_idx);
+    a.knn_d2 = L.at<float>(ws, L.knn_d2);
+    a.rev_cnt = L.at<int32_t>(ws, L.rev_cnt);
+    a.rev_idx = L.at<int32_t>(ws, L.rev_idx);
+    a.rev_d2 = L.at<float>(ws, L.rev_d2);
+    a.ovf = L.at<int32_t>(ws, L.ovf);
+    a.status = L.at<int32_t>(ws, L.status);
+    a.eps = L.at<float>(ws, L.eps);
+    a.tmp_col = L.at<int32_t>(ws, L.tmp_col);
+    a.tmp_d2 = L.at<float>(ws, L.tmp_d2);
+    a.row_start = L.at<int32_t>(ws, L.row_start);
+    a.row_len = L.at<int32_t>(ws, L.row_len);
+    a.col = L.at<int32_t>(ws, L.col);
+    a.w = L.at<float>(ws, L.w);
+    a.d2e = L.at<float>(ws, L.d2e);
+    a.deg = L.at<float>(ws, L.deg);
+    a.ucnt = L.at<int32_t>(ws, L.ucnt);
+    a.diag = L.at<float>(ws, L.diag);
+    a.rhs = L.at<float>(ws, L.rhs);
+    a.P = L.at<float>(ws, L.P);
+    a.Wadj = L.at<float>(ws, L.Wadj);
+    dim3 grid((L.n + 3) / 4);
+    prof_begin(GLL_K_FINALIZE, s);
+    if (y_dtype == GLL_DT_F32) row_build_kernel<float><<<grid, 256, 0, s>>>(a, static_cast<const float*>(Y));
+    else if (y_dtype == GLL_DT_F64) row_build_kernel<double><<<grid, 256, 0, s>>>(a, static_cast<const double*>(Y));
+    else if (y_dtype == GLL_DT_I64) row_build_kernel<int64_t><<<grid, 256, 0, s>>>(a, static_cast<const int64_t*>(Y));
+    else return hipErrorInvalidValue;
+    prof_end(GLL_K_FINALIZE, s);
+    return hipGetLastError();
+}
+
+}  // namespace gll

@@ -50,30 +50,66 @@ __device__ __forceinline__ void block_sum2(float& a, float& b, float* red, int& 
 }
 
 
+// Exclusive prefix sum of one int per thread over the block; `total` gets the block sum.
+template <int NT>
+__device__ __forceinline__ int block_excl_scan(int v, int* scratch, int& total) {
+    const int lane = lane_id();
+    int incl = v;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const int t = __shfl_up(incl, off);
+        if (lane >= off) incl += t;
+    }
+    if constexpr (NT == kWave) {
+        total = __shfl(incl, kWave - 1);
+        return incl - v;
+    } else {
+        constexpr int NW = NT / kWave;
+        const int w = threadIdx.x >> 6;
+        if (lane == kWave - 1) scratch[w] = incl;
+        __syncthreads();
+        int before = 0, all = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            const int sw = scratch[q];
+            before += q < w ? sw : 0;
+            all += sw;
+        }
+        total = all;
+        return before + incl - v;
+    }
+}
+
 template <int NT, int R, int S, typename TB>
 __global__ __launch_bounds__(NT) void cg_ell_kernel(
-    int m, int C, int base, const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ ucnt,
+    int m, int C, int base, const int32_t* __restrict__ row_start,
+    const int32_t* __restrict__ row_len, const int32_t* __restrict__ ucnt,
     const int32_t* __restrict__ col, const float* __restrict__ wv, const float* __restrict__ diag,
     const TB* __restrict__ bsrc, double* __restrict__ out64, float* __restrict__ out32,
-    float rtol, int max_iter, int32_t* __restrict__ st_nonconv, int32_t* __restrict__ st_iters) {
+    float rtol, int max_iter, int mat_cap, int32_t* __restrict__ st_nonconv,
+    int32_t* __restrict__ st_iters) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
-    float* red = smem;        // 4 x 16 floats of reduction scratch
-    float* P_ = smem + 64;    // search direction, gathered by every thread
+    float* red = smem;                                  // 4 x 16 floats of reduction scratch
+    int* scan = reinterpret_cast<int*>(smem + 64);      // 16 ints of scan scratch
+    float* P_ = smem + 128;                             // search direction (gathered)
+    int* lcol = reinterpret_cast<int*>(P_ + ((m + 3) & ~3));   // overflow entries, compacted
+    float* lw = reinterpret_cast<float*>(lcol + mat_cap);
     int ec[R][S];
     float ew[R][S];
     int ost[R], olen[R];
     float x[R], r[R], p[R], ap[R], mi[R], dg[R];
     float rz = 0.f, bb = 0.f;
+    int tov = 0;
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int u = tid + NT * q;
         int len = 0, st = 0;
         x[q] = r[q] = p[q] = ap[q] = mi[q] = dg[q] = 0.f;
         if (u < m) {
-            len = ucnt[u];
-            st = row_ptr[base + u + 1] - len;
+            len = ucnt[u];   // U block = sorted suffix of graph row base + u
+            st = row_start[base + u] + row_len[base + u] - len;
         }
 #pragma unroll
         for (int s = 0; s < S; ++s) {   // ELL slice: independent loads, padded with (0, 0)
@@ -86,6 +122,7 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
         }
         ost[q] = st + S;
         olen[q] = len - S;
+        tov += olen[q] > 0 ? olen[q] : 0;
         if (u < m) {
             dg[q] = diag[u];
             mi[q] = dg[q] > 0.f ? 1.f / dg[q] : 0.f;
@@ -95,6 +132,24 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
             P_[u] = p[q];
             rz += r[q] * p[q];
             bb += r[q] * r[q];
+        }
+    }
+    // entries beyond the ELL slices: compact them into LDS when they fit
+    int ov_total = 0;
+    int ooff = block_excl_scan<NT>(tov, scan, ov_total);
+    const bool matl = ov_total <= mat_cap;
+    if (matl) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            for (int t = 0; t < olen[q]; ++t) {
+                const int e = ost[q] + t;
+                lcol[ooff + t] = col[e] - base;
+                lw[ooff + t] = wv[e];
+            }
+            if (olen[q] > 0) {
+                ost[q] = ooff;
+                ooff += olen[q];
+            }
         }
     }
     int phase = 0;
@@ -111,9 +166,16 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
             float acc = 0.f;
 #pragma unroll
             for (int s = 0; s < S; ++s) acc += ew[q][s] * P_[ec[q][s]];
-            for (int t = 0; t < olen[q]; ++t) {
-                const int e = ost[q] + t;
-                acc += wv[e] * P_[col[e] - base];
+            if (matl) {
+                for (int t = 0; t < olen[q]; ++t) {
+                    const int e = ost[q] + t;
+                    acc += lw[e] * P_[lcol[e]];
+                }
+            } else {
+                for (int t = 0; t < olen[q]; ++t) {
+                    const int e = ost[q] + t;
+                    acc += wv[e] * P_[col[e] - base];
+                }
             }
             ap[q] = dg[q] * p[q] - acc;   // (Luu p)_u = (deg_u + tau) p_u - sum_j W_uj p_j
             pap += p[q] * ap[q];
@@ -161,7 +223,9 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
 // Large systems: vectors in LDS (<= 160 KiB) or in the workspace.
 template <int NT, typename TB>
 __global__ __launch_bounds__(NT) void cg_lds_kernel(
-    int m, int C, int base, const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    int m, int C, int base, const int32_t* __restrict__ row_start,
+    const int32_t* __restrict__ row_len, const int32_t* __restrict__ ucnt,
+    const int32_t* __restrict__ col,
     const float* __restrict__ wv, const float* __restrict__ diag, const TB* __restrict__ bsrc,
     double* __restrict__ out64, float* __restrict__ out32, float rtol, int max_iter,
     float* __restrict__ gvec, int vec_in_lds, int32_t* __restrict__ st_nonconv,
@@ -196,12 +260,9 @@ __global__ __launch_bounds__(NT) void cg_lds_kernel(
         float pap = 0.f, unused = 0.f;
         for (int u = tid; u < m; u += NT) {
             const int i = base + u;
+            const int end = row_start[i] + row_len[i];
             float acc = 0.f;
-            for (int e = row_ptr[i + 1] - 1; e >= row_ptr[i]; --e) {
-                const int j = col[e] - base;
-                if (j < 0) break;
-                acc += wv[e] * P_[j];
-            }
+            for (int e = end - ucnt[u]; e < end; ++e) acc += wv[e] * P_[col[e] - base];
             const float ap = diag[u] * P_[u] - acc;
             A_[u] = ap;
             pap += P_[u] * ap;
@@ -242,11 +303,21 @@ template <int NT, int R, int S, typename TB>
 static hipError_t run_ell(const Layout& L, void* ws, const TB* b, double* out64, float* out32,
                           float rtol, int max_iter, int32_t* st_nonconv, int32_t* st_iters,
                           hipStream_t s) {
-    const size_t lds = 64 * 4 + size_t((L.m + 3) & ~3) * 4;
-    cg_ell_kernel<NT, R, S, TB><<<L.C, NT, lds, s>>>(
-        L.m, L.C, L.base, L.at<int32_t>(ws, L.row_ptr), L.at<int32_t>(ws, L.ucnt),
-        L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w), L.at<float>(ws, L.diag), b, out64, out32,
-        rtol, max_iter, st_nonconv, st_iters);
+    size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4;
+    // entries past the ELL slices: at most (m + n)(K-1) U-block entries in all
+    const int64_t eu_bound = int64_t(L.m + L.n) * (L.K - 1);
+    int64_t cap = int64_t(kLdsLimit - lds) / 8;
+    if (cap > eu_bound) cap = eu_bound;
+    if (cap < 0) cap = 0;
+    lds += size_t(cap) * 8;
+    auto fn = cg_ell_kernel<NT, R, S, TB>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    fn<<<L.C, NT, lds, s>>>(L.m, L.C, L.base, L.at<int32_t>(ws, L.row_start),
+                            L.at<int32_t>(ws, L.row_len), L.at<int32_t>(ws, L.ucnt),
+                            L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
+                            L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, int(cap),
+                            st_nonconv, st_iters);
     return hipGetLastError();
 }
 
@@ -257,13 +328,13 @@ static hipError_t cg_dispatch(const Layout& L, void* ws, const TB* b, double* ou
     const int m = L.m;
 #define GLL_ELL(NT, R, S) \
     return run_ell<NT, R, S, TB>(L, ws, b, out64, out32, rtol, max_iter, st_nonconv, st_iters, s)
-    if (m <= 64) GLL_ELL(64, 1, 16);
-    if (m <= 128) GLL_ELL(128, 1, 16);
-    if (m <= 256) GLL_ELL(256, 1, 16);
-    if (m <= 512) GLL_ELL(512, 1, 16);
+    if (m <= 64) GLL_ELL(64, 1, 24);
+    if (m <= 128) GLL_ELL(128, 1, 24);
+    if (m <= 256) GLL_ELL(256, 1, 24);
+    if (m <= 512) GLL_ELL(512, 1, 24);
     if (m <= 1024) GLL_ELL(1024, 1, 16);
     if (m <= 2048) GLL_ELL(1024, 2, 8);
-    if (m <= 4096) GLL_ELL(1024, 4, 6);
+    if (m <= 4096) GLL_ELL(1024, 4, 4);
 #undef GLL_ELL
     const size_t vec_bytes = size_t(5) * m * sizeof(float);
     const bool vec_lds = 64 * 4 + vec_bytes <= kLdsLimit;
@@ -271,7 +342,8 @@ static hipError_t cg_dispatch(const Layout& L, void* ws, const TB* b, double* ou
     auto fn = cg_lds_kernel<1024, TB>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-    fn<<<L.C, 1024, lds, s>>>(m, L.C, L.base, L.at<int32_t>(ws, L.row_ptr),
+    fn<<<L.C, 1024, lds, s>>>(m, L.C, L.base, L.at<int32_t>(ws, L.row_start),
+                              L.at<int32_t>(ws, L.row_len), L.at<int32_t>(ws, L.ucnt),
                               L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
                               L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter,
                               L.at<float>(ws, L.cgv), vec_lds ? 1 : 0, st_nonconv, st_iters);

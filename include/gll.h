@@ -52,6 +52,9 @@ typedef struct gll_problem {
     float eps;        /* > 0: fixed epsilon (GLL.py:226); <= 0: 'auto' (GLL.py:200-205) */
     float rtol;       /* CG stop: ||r_c|| <= rtol ||b_c|| per column; 0 => 1e-6 */
     int32_t flags;    /* reserved, 0 */
+    int32_t* status_sink; /* optional device words (GLL_ST_NWORDS): when non-NULL the public
+                           * status words accumulate there across calls (sticky; the caller
+                           * reads and clears them when it likes) instead of the workspace */
 } gll_problem;
 
 /* Bytes of device workspace one forward+backward pair needs. */
@@ -82,7 +85,8 @@ typedef struct gll_view {
     int32_t* knn_idx;  /* n x K  neighbour indices, self first, ascending distance */
     float* knn_d2;     /* n x K  squared distances (fp32, exact difference form)    */
     float* eps;        /* n      epsilon_i                                           */
-    int32_t* row_ptr;  /* n + 1  CSR of the symmetric kNN graph (no diagonal)       */
+    int32_t* row_start; /* n     first entry of graph row i (symmetric kNN graph,   */
+    int32_t* row_len;   /* n     no diagonal); entries row_start..+row_len          */
     int32_t* col;      /* E      column indices, ascending within a row             */
     float* w;          /* E      W_ij = exp(-4 d_ij^2 / (eps_i eps_j))               */
     float* d2;         /* E      d_ij^2                                              */
@@ -109,16 +113,13 @@ int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const f
 /* Instrumentation for bench.py: when enabled, every launch of kernel `kid` is bracketed
  * by HIP events on its stream; gll_prof_read synchronises those events and returns the
  * summed milliseconds and the launch count, then clears them. */
-#define GLL_K_GRAM 0
-#define GLL_K_SELECT 1
-#define GLL_K_MUTUAL 2
-#define GLL_K_SCAN 3
-#define GLL_K_FILL 4
-#define GLL_K_FINALIZE 5
-#define GLL_K_CG 6
-#define GLL_K_EDGE 7
-#define GLL_K_GRAD 8
-#define GLL_K_COUNT 9
+#define GLL_K_GRAM 0      /* gram_d2_kernel: fp32 MFMA squared distances */
+#define GLL_K_SELECT 1    /* knn_select_kernel: top-K + exact re-rank + reverse scatter */
+#define GLL_K_FINALIZE 2  /* row_build_kernel: symmetric rows, W, degree, rhs */
+#define GLL_K_CG 3        /* cg_*_kernel: Jacobi-CG solves (forward and adjoint) */
+#define GLL_K_EDGE 4      /* edge_coef_kernel: auto-eps edge coefficients */
+#define GLL_K_GRAD 5      /* grad_spmm_kernel: feature gradient */
+#define GLL_K_COUNT 6
 int gll_prof_enable(int kid, int on);
 int gll_prof_read(int kid, double* ms_total, int* count);
 const char* gll_kernel_name(int kid);

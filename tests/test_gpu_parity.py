@@ -178,13 +178,18 @@ def test_no_labeled_rows_gives_zero_predictions():
     assert U.shape == (128, 10) and torch.count_nonzero(U) == 0
 
 
-def test_status_words_and_iterations():
-    from graphlearninglayer_amd import GLL
-    c = Case("ns_eps1p0_tau0p07_f32")
-    X = torch.from_numpy(c.X).cuda()
-    U = GLL.LaplaceLearningSparseHard.apply(X, torch.from_numpy(c.Y).cuda(), c.tau, c.eps, c.k)
-    torch.cuda.synchronize()
-    GLL._poll_status(block=True)
+def test_status_sink_raises_reference_warning():
+    """Duplicate points make eps_i = 0 in auto mode: the reference warns (GLL.py:240-241)."""
+    GLL = _gll()
+    c = Case("plumbing_epsauto_tau0p07_f32")
+    GLL.check_status()
+    X = c.X.copy()
+    X[70:80] = X[70]          # ten identical rows: their 4th neighbour is at distance 0
+    Xt = torch.from_numpy(X).cuda()
+    GLL.LaplaceLearningSparseHard.apply(Xt, torch.from_numpy(c.Y).cuda(), 0.07, "auto", 5)
+    with pytest.warns(UserWarning, match="very close to zero"):
+        GLL.check_status()
+    U = GLL.LaplaceLearningSparseHard.apply(Xt, torch.from_numpy(c.Y).cuda(), 0.07, 1.0, 5)
     assert torch.isfinite(U).all()
 
 

@@ -36,9 +36,9 @@ def test_library_is_gfx950_code_object():
 def test_problem_struct_matches_header():
     src = open(os.path.join(ROOT, "include", "gll.h")).read()
     body = src[src.index("typedef struct gll_problem"):src.index("} gll_problem;")]
-    fields = re.findall(r"(int32_t|float)\s+(\w+);", body)
+    fields = re.findall(r"(int32_t\*?|float)\s+(\w+);", body)
     assert [f for _, f in fields] == [f for f, _ in _lib.Problem._fields_]
-    assert ct.sizeof(_lib.Problem) == 4 * len(fields)
+    assert ct.sizeof(_lib.Problem) == 4 * (len(fields) - 1) + 8   # 10 words + one pointer
 
 
 def test_view_struct_matches_header():
@@ -76,7 +76,8 @@ def test_entry_points_reject_bad_arguments_without_touching_the_gpu():
 def test_kernel_names():
     names = [_lib.kernel_name(k) for k in range(_lib.K_COUNT)]
     assert names[_lib.K_GRAM] == "gram_d2_kernel"
-    assert names[_lib.K_CG] == "cg_luu_kernel"
+    assert names[_lib.K_CG] == "cg_kernel"
+    assert names[_lib.K_FINALIZE] == "row_build_kernel"
 
 
 def test_eps_and_problem_mapping():
