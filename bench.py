@@ -32,6 +32,7 @@ from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth  #
 METRIC = "GLL fwd+bwd calls/sec (base=500,batch=500,d=512,k=10) at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 MFMA_F32_PEAK_TFS = 157.3    # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), spec
+PROF_PERIOD = 8              # event-bracket every 8th launch of the dominant kernel
 EPS = {"plumbing": 1.0, "ns": 1.0, "fullysup": 1.0, "stress": "auto"}
 TAU = {"plumbing": 0.07, "ns": 0.07, "fullysup": 0.07, "stress": 0.07}
 
@@ -128,19 +129,20 @@ def main():
     dominant = None
     if not a.no_profile:
         for q in range(_lib.K_COUNT):
-            _lib.prof_enable(q, True)
+            _lib.prof_enable(q, 1)
         for _ in range(10):
             step()
         torch.cuda.synchronize()
         for q in range(_lib.K_COUNT):
             ms, cnt = _lib.prof_read(q)
-            _lib.prof_enable(q, False)
+            _lib.prof_enable(q, 0)
             if cnt:
                 per_kernel[names[q]] = {"us_per_launch": round(1e3 * ms / cnt, 3),
                                         "launches_per_step": cnt / 10}
         dominant = max(per_kernel, key=lambda kn: per_kernel[kn]["us_per_launch"]
                        * per_kernel[kn]["launches_per_step"])
-        _lib.prof_enable(names.index(dominant), True)
+        # inside the timed region: bracket every PROF_PERIOD-th launch of the dominant kernel
+        _lib.prof_enable(names.index(dominant), PROF_PERIOD)
 
     # timed region
     if world > 1:
@@ -161,7 +163,7 @@ def main():
     roofline = None
     if dominant is not None:
         ms, cnt = _lib.prof_read(names.index(dominant))
-        _lib.prof_enable(names.index(dominant), False)
+        _lib.prof_enable(names.index(dominant), 0)
         g = GLL.device_graph(X.detach(), k, eps)
         rp = g["row_ptr"].cpu().numpy()
         col = g["col"].cpu().numpy()

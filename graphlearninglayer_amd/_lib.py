@@ -96,8 +96,9 @@ def kernel_name(kid: int) -> str:
     return lib().gll_kernel_name(kid).decode()
 
 
-def prof_enable(kid: int, on: bool = True):
-    check(lib().gll_prof_enable(kid, 1 if on else 0), "gll_prof_enable")
+def prof_enable(kid: int, period: int = 1):
+    """Bracket every `period`-th launch of kernel `kid` with HIP events (0 disables)."""
+    check(lib().gll_prof_enable(kid, int(period)), "gll_prof_enable")
 
 
 def prof_read(kid: int):

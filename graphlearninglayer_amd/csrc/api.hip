@@ -16,6 +16,9 @@ namespace gll {
 // them to time the dominant kernel inside its timed region).
 // ---------------------------------------------------------------------------------------
 struct ProfState {
+    int period[GLL_K_COUNT] = {};     // 0 = off, p = bracket every p-th launch
+    long count[GLL_K_COUNT] = {};
+    bool armed[GLL_K_COUNT] = {};
     bool on[GLL_K_COUNT] = {};
     std::vector<hipEvent_t> pending[GLL_K_COUNT];  // start, stop, start, stop, ...
     std::vector<hipEvent_t> pool;
@@ -36,6 +39,8 @@ static ProfState g_prof;
 void prof_begin(int kid, hipStream_t s) {
     if (!g_prof.on[kid]) return;
     std::lock_guard<std::mutex> lk(g_prof.mu);
+    g_prof.armed[kid] = (g_prof.count[kid]++ % g_prof.period[kid]) == 0;
+    if (!g_prof.armed[kid]) return;
     hipEvent_t e = g_prof.get();
     if (!e) return;
     (void)hipEventRecord(e, s);
@@ -45,6 +50,8 @@ void prof_begin(int kid, hipStream_t s) {
 void prof_end(int kid, hipStream_t s) {
     if (!g_prof.on[kid]) return;
     std::lock_guard<std::mutex> lk(g_prof.mu);
+    if (!g_prof.armed[kid]) return;
+    g_prof.armed[kid] = false;
     if (g_prof.pending[kid].size() % 2 == 0) return;  // begin was not recorded
     hipEvent_t e = g_prof.get();
     if (!e) {
@@ -186,9 +193,13 @@ int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const f
 
 size_t gll_cg_csr_workspace_bytes(int m, int C) { return size_t(5) * m * C * sizeof(float); }
 
-int gll_prof_enable(int kid, int on) {
-    if (kid < 0 || kid >= GLL_K_COUNT) return GLL_ERR_INVALID_ARG;
-    g_prof.on[kid] = on != 0;
+int gll_prof_enable(int kid, int period) {
+    if (kid < 0 || kid >= GLL_K_COUNT || period < 0) return GLL_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    g_prof.on[kid] = period > 0;
+    g_prof.period[kid] = period > 0 ? period : 1;
+    g_prof.count[kid] = 0;
+    g_prof.armed[kid] = false;
     return GLL_OK;
 }
 

@@ -99,19 +99,26 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
                 cf = edge_gv(a, i, cj, a.w[e], ei, g);
             }
         }
-        // lanes own feature columns: accumulate coef_e * x_j in edge order
+        // lanes own feature columns: accumulate coef_e * x_j in edge order, EB rows of X in
+        // flight per batch (padded slots carry coefficient 0 on row i itself)
         const int cnt = min(kWave, end - e0);
-
-        for (int t = 0; t < cnt; ++t) {
-            const float s = readlane_f(cf, t);
-            const int j = readlane_i(cj, t);
-            csum += s;
-            const float* xj = X + size_t(j) * d;
+        constexpr int EB = ND <= 2 ? 4 : (ND <= 4 ? 2 : 1);
+        for (int t0 = 0; t0 < cnt; t0 += EB) {
+            float s[EB];
+            f32x4 v[EB][ND];
 #pragma unroll
-            for (int q = 0; q < ND; ++q) {
-                const int k = 4 * lane + 4 * kWave * q;
-                const f32x4 v = load4<VEC>(xj, k, d);
-                acc[q] += s * v;
+            for (int u = 0; u < EB; ++u) {
+                const int t = t0 + u < cnt ? t0 + u : t0;
+                s[u] = t0 + u < cnt ? readlane_f(cf, t) : 0.f;
+                const float* xj = X + size_t(readlane_i(cj, t)) * d;
+#pragma unroll
+                for (int q = 0; q < ND; ++q) v[u][q] = load4<VEC>(xj, 4 * lane + 4 * kWave * q, d);
+            }
+#pragma unroll
+            for (int u = 0; u < EB; ++u) {
+                csum += s[u];
+#pragma unroll
+                for (int q = 0; q < ND; ++q) acc[q] += s[u] * v[u][q];
             }
         }
     }

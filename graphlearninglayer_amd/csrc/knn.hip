@@ -1,10 +1,10 @@
 // knn.hip -- exact brute-force kNN for the GLL graph (replaces the annoy search of
 // graphlearning.weightmatrix.knnsearch, /root/reference/GLL.py:183).
 //
-//  K1a gram_d2_kernel   D2 = |x_i|^2 + |x_j|^2 - 2 X X^T  on fp32 MFMA (v_mfma_f32_32x32x2_f32)
-//                       64x64 output tile per 256-thread workgroup, one 32x32 tile per wave,
-//                       operands streamed straight to VGPRs (the f32 MFMA needs one VGPR per
-//                       operand per lane), row norms accumulated from the same loads.
+//  K1a gram_sym_kernel  D2 = |x_i|^2 + |x_j|^2 - 2 X X^T on fp32 MFMA (v_mfma_f32_32x32x2_f32),
+//                       upper-triangle 64x64 tiles only (mirrored writes), split-K over two
+//                       wave groups, operands streamed straight to VGPRs (the f32 MFMA needs
+//                       one VGPR per operand per lane), row norms from the same loads.
 //  K1b knn_select_kernel one wave per row:
 //                       1. per-lane sorted candidate lists over the D2 row (16-B loads);
 //                       2. a 64-lane merge to kc = K-1+margin candidates, one DPP arg-min of
@@ -24,75 +24,139 @@
 namespace gll {
 
 // --------------------------------------------------------------------------------------
-// K1a: Gram / squared-distance tile
+// K1a: symmetric Gram tile.  D2 is symmetric, so only tiles bi <= bj are computed and the
+// off-diagonal ones are written twice (D2[i][j] and D2[j][i] bitwise equal).  512 threads:
+// waves 0-3 and 4-7 split the feature dimension in halves (split-K inside the workgroup,
+// combined through LDS in a fixed order), each wave a 32x32 quadrant of the 64x64 tile, with
+// a 3-deep register ring of 32-k chunks in flight ahead of the MFMAs.  The finished tile is
+// staged in LDS so both orientations leave as coalesced 16-B row stores.
 // --------------------------------------------------------------------------------------
-template <bool VEC>
-__global__ __launch_bounds__(256) void gram_d2_kernel(const float* __restrict__ X, int n, int d,
-                                                      float* __restrict__ D2, int ld,
-                                                      int32_t* __restrict__ status,
-                                                      int32_t* __restrict__ rev_cnt) {
-    const int lane = lane_id();
-    const int wave = threadIdx.x >> 6;
-    const int r = lane & 31;   // A row / B column owned by this lane
-    const int h = lane >> 5;   // k half: lane holds k = k0 + 4h + t, t = 0..3
-    const int row0 = blockIdx.y * 64 + (wave >> 1) * 32;
-    const int col0 = blockIdx.x * 64 + (wave & 1) * 32;
-    // per-call reset of the counters the select kernel accumulates into
-    {
-        const int g = (blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
-        if (g < GLL_ST_NWORDS) status[g] = 0;
-        for (int q = g; q < n; q += gridDim.x * gridDim.y * 256) rev_cnt[q] = 0;
-    }
+constexpr int kGramRing = 3;
 
+template <bool VEC>
+__device__ __forceinline__ void gram_chunk_load(const float* pa, const float* pb, int k, int lim,
+                                                f32x4 (&a)[4], f32x4 (&b)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        a[u] = load4<VEC>(pa, k + 8 * u, lim);
+        b[u] = load4<VEC>(pb, k + 8 * u, lim);
+    }
+}
+
+__device__ __forceinline__ void gram_chunk_mfma(const f32x4 (&a)[4], const f32x4 (&b)[4],
+                                                f32x16& acc, float& sa, float& sb) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        sa += a[u].x * a[u].x + a[u].y * a[u].y + a[u].z * a[u].z + a[u].w * a[u].w;
+        sb += b[u].x * b[u].x + b[u].y * b[u].y + b[u].z * b[u].z + b[u].w * b[u].w;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].x, b[u].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].y, b[u].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].z, b[u].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].w, b[u].w, acc, 0, 0, 0);
+    }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(512) void gram_sym_kernel(const float* __restrict__ X, int n, int d,
+                                                       int T, float* __restrict__ D2, int ld,
+                                                       int32_t* __restrict__ status,
+                                                       int32_t* __restrict__ rev_cnt) {
+    __shared__ float s_part[4][16][64];   // k-half 1 partial accumulators, per quadrant
+    __shared__ float s_norm[2][4][64];    // k-half 1 partial row norms (a, b) per quadrant
+    __shared__ float s_tile[64][65];      // finished tile, padded rows
+    __shared__ float s_sq[2][64];         // full squared norms of the tile's rows / columns
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int wave = tid >> 6;
+    const int kh = wave >> 2;             // feature half
+    const int qd = wave & 3;              // quadrant
+    const int r = lane & 31, h = lane >> 5;
+    // upper-triangle tile (bi <= bj) from the linear block id
+    int bi = 0, rem = blockIdx.x;
+    while (rem >= T - bi) {
+        rem -= T - bi;
+        ++bi;
+    }
+    const int bj = bi + rem;
+    {   // per-call reset of the counters the select kernel accumulates into
+        const int g = blockIdx.x * 512 + tid;
+        if (g < GLL_ST_NWORDS) status[g] = 0;
+        for (int q = g; q < n; q += gridDim.x * 512) rev_cnt[q] = 0;
+    }
+    const int row0 = bi * 64 + (qd >> 1) * 32;
+    const int col0 = bj * 64 + (qd & 1) * 32;
+    const int dh = ((d + 63) / 64) * 32;  // feature half, multiple of 32
+    const int k_lo = kh * dh;
+    const int k_hi = min(d, k_lo + dh);
     const float* pa = X + size_t(min(row0 + r, n - 1)) * d + 4 * h;
     const float* pb = X + size_t(min(col0 + r, n - 1)) * d + 4 * h;
-    const int lim = d - 4 * h;
+    const int lim = k_hi - 4 * h;
 
     f32x16 acc;
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = 0.f;
     float sa = 0.f, sb = 0.f;
-
-    constexpr int U = 4;  // 4 steps x 8 k = 32 k per chunk, one chunk prefetched ahead
-    f32x4 a[U], b[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        a[u] = load4<VEC>(pa, 8 * u, lim);
-        b[u] = load4<VEC>(pb, 8 * u, lim);
+    f32x4 a0[4], b0[4], a1[4], b1[4], a2[4], b2[4];
+    gram_chunk_load<VEC>(pa, pb, k_lo, lim, a0, b0);
+    gram_chunk_load<VEC>(pa, pb, k_lo + 32, lim, a1, b1);
+    gram_chunk_load<VEC>(pa, pb, k_lo + 64, lim, a2, b2);
+    for (int k0 = k_lo; k0 < k_hi; k0 += 96) {
+        gram_chunk_mfma(a0, b0, acc, sa, sb);
+        gram_chunk_load<VEC>(pa, pb, k0 + 96, lim, a0, b0);
+        if (k0 + 32 >= k_hi) break;
+        gram_chunk_mfma(a1, b1, acc, sa, sb);
+        gram_chunk_load<VEC>(pa, pb, k0 + 128, lim, a1, b1);
+        if (k0 + 64 >= k_hi) break;
+        gram_chunk_mfma(a2, b2, acc, sa, sb);
+        gram_chunk_load<VEC>(pa, pb, k0 + 160, lim, a2, b2);
     }
-    for (int k0 = 0; k0 < d; k0 += 8 * U) {
-        f32x4 an[U], bn[U];
+    // combine the two feature halves (half 0 + half 1, fixed order)
+    if (kh == 1) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            an[u] = load4<VEC>(pa, k0 + 8 * U + 8 * u, lim);
-            bn[u] = load4<VEC>(pb, k0 + 8 * U + 8 * u, lim);
-        }
+        for (int g = 0; g < 16; ++g) s_part[qd][g][lane] = acc[g];
+        s_norm[0][qd][lane] = sa;
+        s_norm[1][qd][lane] = sb;
+    }
+    __syncthreads();
+    if (kh == 0) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            sa += a[u].x * a[u].x + a[u].y * a[u].y + a[u].z * a[u].z + a[u].w * a[u].w;
-            sb += b[u].x * b[u].x + b[u].y * b[u].y + b[u].z * b[u].z + b[u].w * b[u].w;
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].x, b[u].x, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].y, b[u].y, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].z, b[u].z, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].w, b[u].w, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            a[u] = an[u];
-            b[u] = bn[u];
+        for (int g = 0; g < 16; ++g) acc[g] += s_part[qd][g][lane];
+        sa += s_norm[0][qd][lane];
+        sb += s_norm[1][qd][lane];
+        sa += __shfl_xor(sa, 32);   // the two k quarters of row r
+        sb += __shfl_xor(sb, 32);
+        if (h == 0) {
+            if ((qd & 1) == 0) s_sq[0][(qd >> 1) * 32 + r] = sa;   // tile rows
+            if ((qd >> 1) == 0) s_sq[1][(qd & 1) * 32 + r] = sb;   // tile columns
         }
     }
-    // full row norms: lanes r and r+32 hold the two k halves of row r
-    sa += __shfl_xor(sa, 32);
-    sb += __shfl_xor(sb, 32);
-    const int j = col0 + r;
-    // C/D layout of the 32x32 MFMA: col = lane & 31, row = (g & 3) + 8 (g >> 2) + 4 (lane >> 5)
+    __syncthreads();
+    if (kh == 0) {
+        // C/D layout of the 32x32 MFMA: col = lane & 31, row = (g&3) + 8(g>>2) + 4(lane>>5)
+        const int tc = (qd & 1) * 32 + r;
+        const float sqc = s_sq[1][tc];
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
-        const int ii = (g & 3) + 8 * (g >> 2) + 4 * h;
-        const float sqi = __shfl(sa, ii);
-        const int i = row0 + ii;
-        if (i < n && j < n) D2[size_t(i) * ld + j] = sqi + sb - 2.f * acc[g];
+        for (int g = 0; g < 16; ++g) {
+            const int tr = (qd >> 1) * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
+            s_tile[tr][tc] = s_sq[0][tr] + sqc - 2.f * acc[g];
+        }
+    }
+    __syncthreads();
+    // coalesced stores: 16 threads per 64-float row, 32 rows per pass
+    const int cr = tid >> 4, cc = (tid & 15) * 4;
+    for (int rr = cr; rr < 64; rr += 32) {
+        const int i = bi * 64 + rr;
+        if (i < n) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (bj * 64 + cc + t < n) D2[size_t(i) * ld + bj * 64 + cc + t] = s_tile[rr][cc + t];
+        }
+        const int jr = bj * 64 + rr;
+        if (bi != bj && jr < n) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (bi * 64 + cc + t < n) D2[size_t(jr) * ld + bi * 64 + cc + t] = s_tile[cc + t][rr];
+        }
     }
 }
 
@@ -122,6 +186,83 @@ __device__ __forceinline__ void list_pop(uint64_t (&key)[KC], bool pop) {
     key[KC - 1] = pop ? ~0ull : key[KC - 1];
 }
 
+// Per-lane scan of row i of D2 into a sorted list of the lane's KC smallest keys; returns
+// how many valid columns the lane saw.
+template <int KC>
+__device__ __forceinline__ int scan_row(const float* __restrict__ row, int n, int i,
+                                        uint64_t (&key)[KC]) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int t = 0; t < KC; ++t) key[t] = ~0ull;
+    int seen = 0;
+    for (int j0 = 4 * lane; j0 < n; j0 += 4 * kWave) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(row + j0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int j = j0 + t;
+            if (j < n && j != i && v[t] == v[t]) {   // NaN rows never enter
+                ++seen;
+                const uint64_t kv = pack_key(v[t], j);
+                if (kv < key[KC - 1]) list_insert<KC>(key, kv);
+            }
+        }
+    }
+    return seen;
+}
+
+// Wave64 minimum of a 32-bit unsigned key through DPP (broadcast result).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_min_u32(uint32_t v) {
+    const uint32_t o = __builtin_amdgcn_update_dpp(0xFFFFFFFFu, v, CTRL, ROW_MASK, 0xf, false);
+    return o < v ? o : v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = dpp_min_u32<0xB1, 0xf>(v);
+    v = dpp_min_u32<0x4E, 0xf>(v);
+    v = dpp_min_u32<0x141, 0xf>(v);
+    v = dpp_min_u32<0x140, 0xf>(v);
+    v = dpp_min_u32<0x142, 0xa>(v);
+    v = dpp_min_u32<0x143, 0xc>(v);
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// Exact merge (fallback): round t hands the t-th smallest (d2, index) key to lane t.
+template <int KC>
+__device__ __forceinline__ int merge_exact(uint64_t (&key)[KC], int kc) {
+    const int lane = lane_id();
+    uint64_t mine = ~0ull;
+    for (int t = 0; t < kc; ++t) {
+        const uint64_t best = wave_min_u64(key[0]);
+        if (lane == t) mine = best;
+        list_pop<KC>(key, best != ~0ull && key[0] == best);
+    }
+    return mine == ~0ull ? -1 : int(uint32_t(mine));
+}
+
+// Fast merge: 32-bit DPP arg-min on (value bits with the lane id in the 6 low bits).  The
+// candidate SET can differ from the exact one only between values within 64 ulp of each
+// other, which the exact re-rank margin absorbs.  Returns true when some lane emptied its
+// list while holding more columns (the set may then miss one): the caller re-runs exactly.
+template <int KS>
+__device__ __forceinline__ bool merge_fast(uint64_t (&key)[KS], int kc, int seen, int& ci) {
+    const int lane = lane_id();
+    int popped = 0;
+    ci = -1;
+    for (int t = 0; t < kc; ++t) {
+        const uint32_t hi = uint32_t(key[0] >> 32);
+        const uint32_t packed = key[0] == ~0ull ? 0xFFFFFFFFu : ((hi & ~63u) | uint32_t(lane));
+        const uint32_t m = wave_min_u32(packed);
+        if (m == 0xFFFFFFFFu) break;
+        const int wl = int(m & 63u);
+        const int idx = __builtin_amdgcn_readlane(int(uint32_t(key[0])), wl);
+        if (lane == t) ci = idx;
+        const bool pop = lane == wl;
+        list_pop<KS>(key, pop);
+        popped += pop ? 1 : 0;
+    }
+    return __ballot(popped == KS && seen > KS) != 0;
+}
+
 template <int KC, bool VEC>
 __global__ __launch_bounds__(256) void knn_select_kernel(
     const float* __restrict__ D2, int ld, const float* __restrict__ X, int n, int d, int K,
@@ -133,30 +274,20 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;  // whole wave
 
-    // 1) per-lane scan of the row
-    uint64_t key[KC];
-#pragma unroll
-    for (int t = 0; t < KC; ++t) key[t] = ~0ull;
+    // 1-2) candidates: short per-lane lists + fast merge, exact re-run when inexact
     const float* row = D2 + size_t(i) * ld;
-    for (int j0 = 4 * lane; j0 < n; j0 += 4 * kWave) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(row + j0);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int j = j0 + t;
-            if (j < n && j != i && v[t] == v[t]) {   // NaN rows never enter
-                const uint64_t kv = pack_key(v[t], j);
-                if (kv < key[KC - 1]) list_insert<KC>(key, kv);
-            }
+    constexpr int KS = KC <= 16 ? 4 : 8;
+    int ci;
+    {
+        uint64_t key[KS];
+        const int seen = scan_row<KS>(row, n, i, key);
+        const bool redo = merge_fast<KS>(key, kc, seen, ci);
+        if (redo) {
+            uint64_t full[KC];
+            scan_row<KC>(row, n, i, full);
+            ci = merge_exact<KC>(full, kc);
         }
     }
-    // 2) merge: round t hands the t-th smallest key to lane t
-    uint64_t mine = ~0ull;
-    for (int t = 0; t < kc; ++t) {
-        const uint64_t best = wave_min_u64(key[0]);
-        if (lane == t) mine = best;
-        list_pop<KC>(key, best != ~0ull && key[0] == best);
-    }
-    const int ci = mine == ~0ull ? -1 : int(uint32_t(mine));
     // 3) exact squared distances, 8 candidates per pass (8 lanes each, across d)
     const int grp = lane >> 3, sub = lane & 7;
     const float* xi = X + size_t(i) * d;
@@ -166,6 +297,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
         const bool live = p0 + grp < kc && j >= 0;
         const float* xj = X + size_t(live ? j : i) * d;
         float part = 0.f;
+#pragma unroll 4
         for (int k = 4 * sub; k < d; k += 32) {
             const f32x4 a = load4<VEC>(xi, k, d);
             const f32x4 bb = load4<VEC>(xj, k, d);
@@ -236,13 +368,14 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
 }
 
 hipError_t launch_gram(const Layout& L, void* ws, const float* X, bool vec, hipStream_t s) {
-    dim3 grid((L.n + 63) / 64, (L.n + 63) / 64);
+    const int T = (L.n + 63) / 64;
+    const int tiles = T * (T + 1) / 2;
     float* D2 = L.at<float>(ws, L.D2);
     int32_t* st = L.at<int32_t>(ws, L.status);
     int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
     prof_begin(GLL_K_GRAM, s);
-    if (vec) gram_d2_kernel<true><<<grid, 256, 0, s>>>(X, L.n, L.d, D2, L.ldD, st, rc);
-    else gram_d2_kernel<false><<<grid, 256, 0, s>>>(X, L.n, L.d, D2, L.ldD, st, rc);
+    if (vec) gram_sym_kernel<true><<<tiles, 512, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc);
+    else gram_sym_kernel<false><<<tiles, 512, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc);
     prof_end(GLL_K_GRAM, s);
     return hipGetLastError();
 }

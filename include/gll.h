@@ -110,9 +110,10 @@ int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const f
                const float* b, float* x, float atol, int max_iter, int32_t* iters,
                int32_t* nonconv, void* workspace, void* stream);
 
-/* Instrumentation for bench.py: when enabled, every launch of kernel `kid` is bracketed
- * by HIP events on its stream; gll_prof_read synchronises those events and returns the
- * summed milliseconds and the launch count, then clears them. */
+/* Instrumentation for bench.py: with period p > 0, every p-th launch of kernel `kid` is
+ * bracketed by HIP events on its stream (p = 0 disables); gll_prof_read synchronises those
+ * events and returns the summed milliseconds and the number of bracketed launches, then
+ * clears them. */
 #define GLL_K_GRAM 0      /* gram_d2_kernel: fp32 MFMA squared distances */
 #define GLL_K_SELECT 1    /* knn_select_kernel: top-K + exact re-rank + reverse scatter */
 #define GLL_K_FINALIZE 2  /* row_build_kernel: symmetric rows, W, degree, rhs */
@@ -120,7 +121,7 @@ int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const f
 #define GLL_K_EDGE 4      /* edge_coef_kernel: auto-eps edge coefficients */
 #define GLL_K_GRAD 5      /* grad_spmm_kernel: feature gradient */
 #define GLL_K_COUNT 6
-int gll_prof_enable(int kid, int on);
+int gll_prof_enable(int kid, int period);
 int gll_prof_read(int kid, double* ms_total, int* count);
 const char* gll_kernel_name(int kid);
 
