@@ -34,4 +34,17 @@ if [[ $STEPS == *pmc* ]]; then
   run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_write_$PROF_CFG" -o run -- \
       python3 "$R/bench.py" --config $PROF_CFG --steps 20 --warmup 5 --cpu-seconds 0 --no-profile
 fi
+if [[ $STEPS == *host* ]]; then
+  run host 300 python tools/host_overhead.py
+fi
+if [[ $STEPS == *ctr* ]]; then
+  export TMPDIR=/tmp
+  R=$PWD
+  run counters_list 120 rocprofv3 -L
+  grep -oE "(GRBM_GUI_ACTIVE|SQ_WAVES|SQ_BUSY_CYCLES|SQ_WAIT_INST_ANY|SQ_WAIT_ANY|SQ_ACTIVE_INST_ANY|SQ_INSTS_VALU|SQ_INSTS_MFMA|SQ_VALU_MFMA_BUSY_CYCLES|SQ_INSTS_VALU_MFMA_MOPS_F32|SQ_WAVE_CYCLES|TA_BUSY_avr|SQ_INSTS_LDS|SQ_LDS_BANK_CONFLICT|SQ_INST_CYCLES_VMEM)[A-Za-z0-9_]*" gpurun_out/counters_list.log | sort -u | head -40
+  run pmc_a 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_a" -o run -- \
+      python3 "$R/bench.py" --steps 20 --warmup 5 --cpu-seconds 0 --no-profile
+  run pmc_b 300 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_b" -o run -- \
+      python3 "$R/bench.py" --steps 20 --warmup 5 --cpu-seconds 0 --no-profile
+fi
 exit 0
