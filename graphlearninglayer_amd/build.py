@@ -70,7 +70,44 @@ def build(force=False, verbose=False, extra=()):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    build_torch_ext(force=force, verbose=verbose)
     return LIB
+
+
+TORCH_EXT_SRC = os.path.join(CSRC, "torch_ext.cpp")
+TORCH_EXT = os.path.join(HERE, "_gll_torch.so")
+
+
+def build_torch_ext(force=False, verbose=False):
+    """The C++ autograd node (csrc/torch_ext.cpp) as a Python extension module linked
+    against libgll.so and libtorch; built in-tree so it travels with the repo."""
+    if (not force and os.path.exists(TORCH_EXT)
+            and os.path.getmtime(TORCH_EXT) >= max(os.path.getmtime(TORCH_EXT_SRC),
+                                                   os.path.getmtime(LIB), _headers_mtime())):
+        return TORCH_EXT
+    import sysconfig
+
+    import torch
+    from torch.utils import cpp_extension
+
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared",
+           "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H",
+           "-DTORCH_EXTENSION_NAME=_gll_torch", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+           *[f"-I{p}" for p in cpp_extension.include_paths()],
+           f"-I{sysconfig.get_paths()['include']}", f"-I{rocm}/include", f"-I{INCLUDE}",
+           TORCH_EXT_SRC, "-o", TORCH_EXT,
+           f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+           "-ltorch_python", f"-L{HERE}", "-lgll", f"-L{rocm}/lib", "-lamdhip64",
+           f"-Wl,-rpath,{tlib}", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"torch extension build failed:\n{r.stdout}\n{r.stderr[-4000:]}")
+    return TORCH_EXT
 
 
 def main():

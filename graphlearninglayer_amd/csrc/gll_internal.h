@@ -168,18 +168,25 @@ template <typename T>
 __device__ __forceinline__ float to_f32(T v) { return static_cast<float>(v); }
 
 // Load 4 consecutive floats p[k..k+3] (zeros beyond `lim`).  VEC: 16-B vector load, needs
-// lim % 4 == 0 and 16-B alignment; otherwise scalar guarded loads.
+// lim % 4 == 0 and 16-B alignment; otherwise scalar loads.  Branch-free: out-of-range lanes
+// load p[0..] (p must be readable) and select zero, so hipcc keeps exact vmcnt counting and
+// prefetches stay in flight (a predicated load becomes a branch + vmcnt(0) drain).
 template <bool VEC>
 __device__ __forceinline__ f32x4 load4(const float* __restrict__ p, int k, int lim) {
     f32x4 v;
     if constexpr (VEC) {
-        if (k < lim) v = *reinterpret_cast<const f32x4*>(p + k);
-        else v = f32x4{0.f, 0.f, 0.f, 0.f};
+        const bool in = k < lim;
+        v = *reinterpret_cast<const f32x4*>(p + (in ? k : 0));
+        v = in ? v : f32x4{0.f, 0.f, 0.f, 0.f};
     } else {
-        v.x = (k + 0 < lim) ? p[k + 0] : 0.f;
-        v.y = (k + 1 < lim) ? p[k + 1] : 0.f;
-        v.z = (k + 2 < lim) ? p[k + 2] : 0.f;
-        v.w = (k + 3 < lim) ? p[k + 3] : 0.f;
+        const float a = p[k + 0 < lim ? k + 0 : 0];
+        const float b = p[k + 1 < lim ? k + 1 : 0];
+        const float c = p[k + 2 < lim ? k + 2 : 0];
+        const float e = p[k + 3 < lim ? k + 3 : 0];
+        v.x = k + 0 < lim ? a : 0.f;
+        v.y = k + 1 < lim ? b : 0.f;
+        v.z = k + 2 < lim ? c : 0.f;
+        v.w = k + 3 < lim ? e : 0.f;
     }
     return v;
 }

@@ -20,11 +20,23 @@
 // the CSR).  Only p is published through LDS for the gathers.  Dot products are DPP wave
 // reductions plus one LDS exchange across waves; an iteration has three barriers.
 // cg_lds_kernel: vectors in LDS or global memory, for systems larger than that.
+#include <mutex>
+#include <unordered_set>
+
 #include "gll_internal.h"
 
 namespace gll {
 
 static constexpr size_t kLdsLimit = 160 * 1024;
+
+// Opt a kernel into the full 160 KiB of dynamic LDS, once per kernel (host-side cost).
+static void allow_full_lds(const void* fn) {
+    static std::mutex mu;
+    static std::unordered_set<const void*> done;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.insert(fn).second)
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsLimit));
+}
 
 // Block-wide sum of two values; every thread gets the totals (fixed order -> deterministic).
 template <int NT>
@@ -311,8 +323,7 @@ static hipError_t run_ell(const Layout& L, void* ws, const TB* b, double* out64,
     if (cap < 0) cap = 0;
     lds += size_t(cap) * 8;
     auto fn = cg_ell_kernel<NT, R, S, TB>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    allow_full_lds(reinterpret_cast<const void*>(fn));
     fn<<<L.C, NT, lds, s>>>(L.m, L.C, L.base, L.at<int32_t>(ws, L.row_start),
                             L.at<int32_t>(ws, L.row_len), L.at<int32_t>(ws, L.ucnt),
                             L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
@@ -340,8 +351,7 @@ static hipError_t cg_dispatch(const Layout& L, void* ws, const TB* b, double* ou
     const bool vec_lds = 64 * 4 + vec_bytes <= kLdsLimit;
     const size_t lds = 64 * 4 + (vec_lds ? vec_bytes : 0);
     auto fn = cg_lds_kernel<1024, TB>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    allow_full_lds(reinterpret_cast<const void*>(fn));
     fn<<<L.C, 1024, lds, s>>>(m, L.C, L.base, L.at<int32_t>(ws, L.row_start),
                               L.at<int32_t>(ws, L.row_len), L.at<int32_t>(ws, L.ucnt),
                               L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
@@ -451,8 +461,7 @@ hipError_t launch_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* co
     if (!vec_lds && gvec == nullptr) return hipErrorInvalidValue;
     const size_t lds = 64 * 4 + (vec_lds ? vec_bytes : 0);
     auto fn = cg_csr_kernel<256>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    allow_full_lds(reinterpret_cast<const void*>(fn));
     prof_begin(GLL_K_CG, s);
     fn<<<C, 256, lds, s>>>(m, C, row_ptr, col, val, b, x, atol, max_iter, gvec, vec_lds ? 1 : 0,
                            iters, nonconv);

@@ -240,3 +240,35 @@ def test_stress_shape_graph_parity():
     Uo, st = O.forward(X, Y, 0.07, "auto", s["k"], knn=(ind, None))
     assert O.rel_err(U, Uo) < TOL
     assert O.rel_err(grad, O.backward(st, gb)) < TOL
+
+
+def test_cpp_node_and_python_function_agree_bitwise():
+    """The C++ autograd node (what .apply runs) and the ctypes Python Function are the
+    same kernels: identical outputs and gradients."""
+    GLL = _gll()
+    assert GLL._ext() is not None
+    c = Case("ns_epsauto_tau0p07_f32")
+    X = torch.from_numpy(c.X).cuda().requires_grad_(True)
+    Y = torch.from_numpy(c.Y).cuda()
+    g = torch.from_numpy(c.gbar).cuda()
+    U1 = GLL.LaplaceLearningSparseHard.apply(X, Y, c.tau, c.eps, c.k)
+    (g1,) = torch.autograd.grad(U1, X, g)
+    U2 = GLL.LaplaceLearningSparseHard.apply_python(X, Y, c.tau, c.eps, c.k)
+    (g2,) = torch.autograd.grad(U2, X, g)
+    assert U1.grad_fn is not None and U2.grad_fn is not None
+    assert torch.equal(U1, U2) and torch.equal(g1, g2)
+
+
+def test_output_does_not_alias_saved_state():
+    """Callers edit the output in place (adversarial.py:691); backward must not change."""
+    GLL = _gll()
+    c = Case("plumbing_eps1p0_tau0p07_f32")
+    X = torch.from_numpy(c.X).cuda().requires_grad_(True)
+    Y = torch.from_numpy(c.Y).cuda()
+    g = torch.from_numpy(c.gbar).cuda()
+    U = GLL.LaplaceLearningSparseHard.apply(X, Y, c.tau, c.eps, c.k)
+    (ref,) = torch.autograd.grad(U, X, g, retain_graph=True)
+    with torch.no_grad():
+        U.mul_(0.5).add_(1.0)
+    (again,) = torch.autograd.grad(U, X, g)
+    assert torch.equal(ref, again)

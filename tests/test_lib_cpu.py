@@ -119,3 +119,10 @@ def test_product_package_never_imports_the_oracle():
                 src = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle\b", src, flags=re.M), f
                 assert "oracle." not in src, f
+
+
+def test_torch_extension_module_loads():
+    from graphlearninglayer_amd import GLL as GG
+    ext = GG._ext()
+    assert ext is not None, "_gll_torch.so missing: run __graft_entry__.build()"
+    assert hasattr(ext, "laplace_learning")
