@@ -1,10 +1,10 @@
 // knn.hip -- exact brute-force kNN for the GLL graph (replaces the annoy search of
 // graphlearning.weightmatrix.knnsearch, /root/reference/GLL.py:183).
 //
-//  K1a gram_sym_kernel  D2 = |x_i|^2 + |x_j|^2 - 2 X X^T on fp32 MFMA (v_mfma_f32_32x32x2_f32),
+//  K1a gram_lds_kernel  D2 = |x_i|^2 + |x_j|^2 - 2 X X^T on fp32 MFMA (v_mfma_f32_32x32x2_f32),
 //                       upper-triangle 64x64 tiles only (mirrored writes), split-K over two
-//                       wave groups, operands streamed straight to VGPRs (the f32 MFMA needs
-//                       one VGPR per operand per lane), row norms from the same loads.
+//                       wave groups, LDS-staged double-buffered k-chunks, row norms from the
+//                       same operands.
 //  K1b knn_select_kernel one wave per row:
 //                       1. per-lane sorted candidate lists over the D2 row (16-B loads);
 //                       2. a 64-lane merge to kc = K-1+margin candidates, one DPP arg-min of
@@ -27,22 +27,10 @@ namespace gll {
 // K1a: symmetric Gram tile.  D2 is symmetric, so only tiles bi <= bj are computed and the
 // off-diagonal ones are written twice (D2[i][j] and D2[j][i] bitwise equal).  512 threads:
 // waves 0-3 and 4-7 split the feature dimension in halves (split-K inside the workgroup,
-// combined through LDS in a fixed order), each wave a 32x32 quadrant of the 64x64 tile, with
-// a 3-deep register ring of 32-k chunks in flight ahead of the MFMAs.  The finished tile is
-// staged in LDS so both orientations leave as coalesced 16-B row stores.
+// combined through LDS in a fixed order), each wave a 32x32 quadrant of the 64x64 tile.
+// The finished tile is staged in LDS so both orientations leave as coalesced row stores.
 // --------------------------------------------------------------------------------------
-constexpr int kGramRing = 3;
-
-template <bool VEC>
-__device__ __forceinline__ void gram_chunk_load(const float* pa, const float* pb, int k, int lim,
-                                                f32x4 (&a)[4], f32x4 (&b)[4]) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        a[u] = load4<VEC>(pa, k + 8 * u, lim);
-        b[u] = load4<VEC>(pb, k + 8 * u, lim);
-    }
-}
-
+// 16 MFMAs over one 32-k chunk: lane (r, h) holds A[r][8u + 4h + t], B[c=r][8u + 4h + t]
 __device__ __forceinline__ void gram_chunk_mfma(const f32x4 (&a)[4], const f32x4 (&b)[4],
                                                 f32x16& acc, float& sa, float& sb) {
 #pragma unroll
@@ -56,22 +44,29 @@ __device__ __forceinline__ void gram_chunk_mfma(const f32x4 (&a)[4], const f32x4
     }
 }
 
+// --------------------------------------------------------------------------------------
+// Every 32-wide k-chunk of the tile's 64 A rows and 64 B rows is fetched once per
+// workgroup with coalesced 16-B loads (8 lanes per 128-B row segment), staged in padded LDS
+// rows (36 floats: conflict-free ds_read_b128 for the MFMA fragments) and double-buffered:
+// chunk c+1 is in registers on its way to LDS while chunk c feeds the MFMAs.
+// --------------------------------------------------------------------------------------
+constexpr int kGBK = 32;        // k per chunk
+constexpr int kGLD = kGBK + 4;  // padded LDS row (floats)
+
 template <bool VEC>
-__global__ __launch_bounds__(512) void gram_sym_kernel(const float* __restrict__ X, int n, int d,
+__global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__ X, int n, int d,
                                                        int T, float* __restrict__ D2, int ld,
                                                        int32_t* __restrict__ status,
                                                        int32_t* __restrict__ rev_cnt) {
-    __shared__ float s_part[4][16][64];   // k-half 1 partial accumulators, per quadrant
-    __shared__ float s_norm[2][4][64];    // k-half 1 partial row norms (a, b) per quadrant
-    __shared__ float s_tile[64][65];      // finished tile, padded rows
-    __shared__ float s_sq[2][64];         // full squared norms of the tile's rows / columns
+    // stage[buf][half][A|B][64 rows][kGLD] ; the epilogue reuses the same storage
+    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * 2 * 64 * kGLD];
+    __shared__ float s_sq[2][64];
     const int tid = threadIdx.x;
     const int lane = lane_id();
     const int wave = tid >> 6;
-    const int kh = wave >> 2;             // feature half
-    const int qd = wave & 3;              // quadrant
+    const int kh = wave >> 2;             // feature half of this wave
+    const int qd = wave & 3;              // 32x32 quadrant of this wave
     const int r = lane & 31, h = lane >> 5;
-    // upper-triangle tile (bi <= bj) from the linear block id
     int bi = 0, rem = blockIdx.x;
     while (rem >= T - bi) {
         rem -= T - bi;
@@ -83,79 +78,108 @@ __global__ __launch_bounds__(512) void gram_sym_kernel(const float* __restrict__
         if (g < GLL_ST_NWORDS) status[g] = 0;
         for (int q = g; q < n; q += gridDim.x * 512) rev_cnt[q] = 0;
     }
-    const int row0 = bi * 64 + (qd >> 1) * 32;
-    const int col0 = bj * 64 + (qd & 1) * 32;
-    const int dh = ((d + 63) / 64) * 32;  // feature half, multiple of 32
+    const int dh = ((d + 2 * kGBK - 1) / (2 * kGBK)) * kGBK;   // per-half span, x32
+    const int nchunk = dh / kGBK;                                // same for both halves
+    // loader role: the 256 threads of half `kh` load that half's chunks.  Thread t loads
+    // rows (t >> 3) and (t >> 3) + 32 of A and B at column 4 (t & 7).
+    const int lt = tid & 255;
+    const int lrow = lt >> 3, lcol = 4 * (lt & 7);
     const int k_lo = kh * dh;
     const int k_hi = min(d, k_lo + dh);
-    const float* pa = X + size_t(min(row0 + r, n - 1)) * d + 4 * h;
-    const float* pb = X + size_t(min(col0 + r, n - 1)) * d + 4 * h;
-    const int lim = k_hi - 4 * h;
-
+    const float* ga0 = X + size_t(min(bi * 64 + lrow, n - 1)) * d;
+    const float* ga1 = X + size_t(min(bi * 64 + lrow + 32, n - 1)) * d;
+    const float* gb0 = X + size_t(min(bj * 64 + lrow, n - 1)) * d;
+    const float* gb1 = X + size_t(min(bj * 64 + lrow + 32, n - 1)) * d;
+    auto stage = [&](int buf, int which) -> float* {
+        return smem + ((buf * 2 + kh) * 2 + which) * 64 * kGLD;
+    };
+    f32x4 la0, la1, lb0, lb1;
+    auto gload = [&](int c) {
+        const int k = k_lo + c * kGBK + lcol;
+        la0 = load4<VEC>(ga0, k, k_hi);
+        la1 = load4<VEC>(ga1, k, k_hi);
+        lb0 = load4<VEC>(gb0, k, k_hi);
+        lb1 = load4<VEC>(gb1, k, k_hi);
+    };
+    auto lstore = [&](int buf) {
+        float* A = stage(buf, 0);
+        float* B = stage(buf, 1);
+        *reinterpret_cast<f32x4*>(A + lrow * kGLD + lcol) = la0;
+        *reinterpret_cast<f32x4*>(A + (lrow + 32) * kGLD + lcol) = la1;
+        *reinterpret_cast<f32x4*>(B + lrow * kGLD + lcol) = lb0;
+        *reinterpret_cast<f32x4*>(B + (lrow + 32) * kGLD + lcol) = lb1;
+    };
     f32x16 acc;
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = 0.f;
     float sa = 0.f, sb = 0.f;
-    f32x4 a0[4], b0[4], a1[4], b1[4], a2[4], b2[4];
-    gram_chunk_load<VEC>(pa, pb, k_lo, lim, a0, b0);
-    gram_chunk_load<VEC>(pa, pb, k_lo + 32, lim, a1, b1);
-    gram_chunk_load<VEC>(pa, pb, k_lo + 64, lim, a2, b2);
-    for (int k0 = k_lo; k0 < k_hi; k0 += 96) {
-        gram_chunk_mfma(a0, b0, acc, sa, sb);
-        gram_chunk_load<VEC>(pa, pb, k0 + 96, lim, a0, b0);
-        if (k0 + 32 >= k_hi) break;
-        gram_chunk_mfma(a1, b1, acc, sa, sb);
-        gram_chunk_load<VEC>(pa, pb, k0 + 128, lim, a1, b1);
-        if (k0 + 64 >= k_hi) break;
-        gram_chunk_mfma(a2, b2, acc, sa, sb);
-        gram_chunk_load<VEC>(pa, pb, k0 + 160, lim, a2, b2);
+    const int arow = (qd >> 1) * 32 + r, brow = (qd & 1) * 32 + r;
+    gload(0);
+    lstore(0);
+    if (nchunk > 1) gload(1);
+    __syncthreads();
+    for (int c = 0; c < nchunk; ++c) {
+        const int buf = c & 1;
+        const float* A = stage(buf, 0) + arow * kGLD + 4 * h;
+        const float* B = stage(buf, 1) + brow * kGLD + 4 * h;
+        f32x4 a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a[u] = *reinterpret_cast<const f32x4*>(A + 8 * u);
+            b[u] = *reinterpret_cast<const f32x4*>(B + 8 * u);
+        }
+        if (c + 1 < nchunk) lstore(buf ^ 1);   // chunk c+1: registers -> LDS (other buffer)
+        if (c + 2 < nchunk) gload(c + 2);      // chunk c+2: HBM/L2 -> registers
+        gram_chunk_mfma(a, b, acc, sa, sb);
+        __syncthreads();
     }
-    // combine the two feature halves (half 0 + half 1, fixed order)
+    // combine the feature halves in a fixed order (half 0 + half 1) through LDS
+    float* part = smem;                    // [4 quadrants][16][64]
+    float* nrm = smem + 4 * 16 * 64;       // [2][4][64]
     if (kh == 1) {
 #pragma unroll
-        for (int g = 0; g < 16; ++g) s_part[qd][g][lane] = acc[g];
-        s_norm[0][qd][lane] = sa;
-        s_norm[1][qd][lane] = sb;
+        for (int g = 0; g < 16; ++g) part[(qd * 16 + g) * 64 + lane] = acc[g];
+        nrm[(0 * 4 + qd) * 64 + lane] = sa;
+        nrm[(1 * 4 + qd) * 64 + lane] = sb;
     }
     __syncthreads();
     if (kh == 0) {
 #pragma unroll
-        for (int g = 0; g < 16; ++g) acc[g] += s_part[qd][g][lane];
-        sa += s_norm[0][qd][lane];
-        sb += s_norm[1][qd][lane];
+        for (int g = 0; g < 16; ++g) acc[g] += part[(qd * 16 + g) * 64 + lane];
+        sa += nrm[(0 * 4 + qd) * 64 + lane];
+        sb += nrm[(1 * 4 + qd) * 64 + lane];
         sa += __shfl_xor(sa, 32);   // the two k quarters of row r
         sb += __shfl_xor(sb, 32);
         if (h == 0) {
-            if ((qd & 1) == 0) s_sq[0][(qd >> 1) * 32 + r] = sa;   // tile rows
-            if ((qd >> 1) == 0) s_sq[1][(qd & 1) * 32 + r] = sb;   // tile columns
+            if ((qd & 1) == 0) s_sq[0][(qd >> 1) * 32 + r] = sa;
+            if ((qd >> 1) == 0) s_sq[1][(qd & 1) * 32 + r] = sb;
         }
     }
     __syncthreads();
+    float* tile = smem + 8 * 16 * 64;      // [64][65], past part/nrm
     if (kh == 0) {
-        // C/D layout of the 32x32 MFMA: col = lane & 31, row = (g&3) + 8(g>>2) + 4(lane>>5)
         const int tc = (qd & 1) * 32 + r;
         const float sqc = s_sq[1][tc];
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
             const int tr = (qd >> 1) * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
-            s_tile[tr][tc] = s_sq[0][tr] + sqc - 2.f * acc[g];
+            tile[tr * 65 + tc] = s_sq[0][tr] + sqc - 2.f * acc[g];
         }
     }
     __syncthreads();
-    // coalesced stores: 16 threads per 64-float row, 32 rows per pass
     const int cr = tid >> 4, cc = (tid & 15) * 4;
     for (int rr = cr; rr < 64; rr += 32) {
         const int i = bi * 64 + rr;
         if (i < n) {
 #pragma unroll
             for (int t = 0; t < 4; ++t)
-                if (bj * 64 + cc + t < n) D2[size_t(i) * ld + bj * 64 + cc + t] = s_tile[rr][cc + t];
+                if (bj * 64 + cc + t < n) D2[size_t(i) * ld + bj * 64 + cc + t] = tile[rr * 65 + cc + t];
         }
         const int jr = bj * 64 + rr;
         if (bi != bj && jr < n) {
 #pragma unroll
             for (int t = 0; t < 4; ++t)
-                if (bi * 64 + cc + t < n) D2[size_t(jr) * ld + bi * 64 + cc + t] = s_tile[cc + t][rr];
+                if (bi * 64 + cc + t < n) D2[size_t(jr) * ld + bi * 64 + cc + t] = tile[(cc + t) * 65 + rr];
         }
     }
 }
@@ -374,8 +398,8 @@ hipError_t launch_gram(const Layout& L, void* ws, const float* X, bool vec, hipS
     int32_t* st = L.at<int32_t>(ws, L.status);
     int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
     prof_begin(GLL_K_GRAM, s);
-    if (vec) gram_sym_kernel<true><<<tiles, 512, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc);
-    else gram_sym_kernel<false><<<tiles, 512, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc);
+    if (vec) gram_lds_kernel<true><<<tiles, 512, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc);
+    else gram_lds_kernel<false><<<tiles, 512, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc);
     prof_end(GLL_K_GRAM, s);
     return hipGetLastError();
 }
