@@ -34,6 +34,9 @@ if [[ $STEPS == *pmc* ]]; then
   run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_write_$PROF_CFG" -o run -- \
       python3 "$R/bench.py" --config $PROF_CFG --steps 20 --warmup 5 --cpu-seconds 0 --no-profile
 fi
+if [[ $STEPS == *scale* ]]; then
+  run scale 600 python tools/scale_probe.py
+fi
 if [[ $STEPS == *host* ]]; then
   run host 300 python tools/host_overhead.py
 fi
