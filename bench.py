@@ -67,6 +67,30 @@ def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps):
     return u
 
 
+# C-ABI kernel ids (gll_kernel_name) -> device symbols as rocprofv3 names them
+PMC_SYMBOLS = {"gram_d2_kernel": ["gram_lds_kernel"], "knn_select_kernel": ["knn_select_kernel"],
+               "row_build_kernel": ["row_build_kernel"],
+               "cg_kernel": ["cg_ell_kernel", "cg_lds_kernel"],
+               "edge_coef_kernel": ["edge_coef_kernel"], "grad_spmm_kernel": ["grad_spmm_kernel"]}
+
+
+def pmc_traffic(config, kernel):
+    """HBM-side bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN_pmc_<config>.json, written by tools/pmc_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command), or None."""
+    import glob
+    here = os.path.dirname(os.path.abspath(__file__))
+    paths = sorted(glob.glob(os.path.join(here, "profiles", f"r*_pmc_{config}.json")))
+    if not paths:
+        return None
+    with open(paths[-1]) as f:
+        doc = json.load(f)
+    for sym in PMC_SYMBOLS.get(kernel, []):
+        if sym in doc["kernels"]:
+            return round(doc["kernels"][sym]["traffic_bytes"], 1)
+    return None
+
+
 def cpu_baseline(cfg, eps, tau, seconds):
     """Time the reference's CPU step sequence (oracle/gll_port.py, 'port') on this host."""
     from oracle import gll_port
@@ -161,6 +185,7 @@ def main():
         elapsed = float(t.item())
 
     roofline = None
+    call_roof_s = None
     if dominant is not None:
         ms, cnt = _lib.prof_read(names.index(dominant))
         _lib.prof_enable(names.index(dominant), 0)
@@ -180,9 +205,14 @@ def main():
             achieved, peak, unit = work / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
         roofline = {"kernel": dominant, "bound": bound, "achieved": round(achieved, 3),
                     "peak": peak, "unit": unit, "frac": round(achieved / peak, 5),
-                    "traffic": None, "work_per_launch": work,
+                    "traffic": pmc_traffic(a.config, dominant), "work_per_launch": work,
                     "avg_launch_us": round(avg_s * 1e6, 3), "launches": cnt,
                     "cg_iters_fwd_bwd": list(iters)}
+        # whole-call roofline: kNN at the MFMA peak + every other byte at HBM
+        f_knn = units["gram_d2_kernel"][1]
+        b_rest = sum(w_ * per_kernel[kn]["launches_per_step"] for kn, (b_, w_) in units.items()
+                     if b_ == "hbm" and kn in per_kernel)
+        call_roof_s = f_knn / (MFMA_F32_PEAK_TFS * 1e12) + b_rest / (HBM_PEAK_GBS * 1e9)
         for kn, v in per_kernel.items():
             b_, w_ = units[kn]
             v["algorithmic"] = (f"{w_ / 1e9:.4g} GFLOP" if b_ == "mfma" else f"{w_ / 1e6:.4g} MB")
@@ -214,6 +244,9 @@ def main():
             "cpu_baseline": cpu,
             "kernels": per_kernel,
         }
+        if roofline is not None:
+            out["call_roofline"] = {"t_roof_us": round(call_roof_s * 1e6, 3),
+                                    "frac": round(call_roof_s / (elapsed / a.steps), 5)}
         if cpu:
             out["speedup_vs_cpu"] = round(out["value"] / cpu["value"], 1)
         print(json.dumps(out), flush=True)

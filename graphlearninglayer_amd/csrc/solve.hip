@@ -114,7 +114,6 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     float x[R], r[R], p[R], ap[R], mi[R], dg[R];
     float rz = 0.f, bb = 0.f;
     int tov = 0;
-    int lmax = 0;   // longest ELL slice of this thread's rows
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int u = tid + NT * q;
@@ -136,7 +135,6 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
         ost[q] = st + S;
         olen[q] = len - S;
         tov += olen[q] > 0 ? olen[q] : 0;
-        lmax = max(lmax, min(len, S));
         if (u < m) {
             dg[q] = diag[u];
             mi[q] = dg[q] > 0.f ? 1.f / dg[q] : 0.f;
@@ -148,12 +146,6 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
             bb += r[q] * r[q];
         }
     }
-    // gathers past the wave's longest slice are skipped (scalar branch): rows hold ~K/2
-    // U entries on average, the slice is sized for the longest rows
-    int wmax = lmax;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, __shfl_xor(wmax, off));
-    wmax = __builtin_amdgcn_readfirstlane(wmax);
     // entries beyond the ELL slices: compact them into LDS when they fit
     int ov_total = 0;
     int ooff = block_excl_scan<NT>(tov, scan, ov_total);
@@ -186,7 +178,7 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
             float acc = 0.f;
 #pragma unroll
             for (int s = 0; s < S; ++s)
-                if (s < wmax) acc += ew[q][s] * P_[ec[q][s]];   // wave-uniform slot bound
+                acc += ew[q][s] * P_[ec[q][s]];
             if (matl) {
                 for (int t = 0; t < olen[q]; ++t) {
                     const int e = ost[q] + t;

@@ -1,0 +1,74 @@
+"""World-size-2 rehearsal of the multi-GPU path on CPU (gloo): SURVEY.md §8e.
+
+Each rank owns an independent minibatch graph (seed = rank), computes its predictions with
+the oracle (the GPU product path is exercised by the -m gpu tests), and all-gathers them the
+way bench.py does; every rank must then hold every other rank's predictions bit-for-bit, and
+the max-over-ranks timing reduction must agree on all ranks.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from graphlearninglayer_amd.parallel import gather_predictions, shard_rank_seed
+from graphlearninglayer_amd.synth import CONFIGS, one_hot, synth
+from oracle import gll_oracle
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _shard_predictions(rank):
+    c = CONFIGS["plumbing"]
+    X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=shard_rank_seed(0, rank))
+    Y = one_hot(lab[: c["base"]])
+    U, _ = gll_oracle.forward(X, Y, tau=0.07, epsilon=1.0, K=c["k"])
+    return torch.from_numpy(np.ascontiguousarray(U, dtype=np.float32))
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        U = _shard_predictions(rank)
+        full, work = gather_predictions(U, async_op=True)
+        assert work is not None
+        work.wait()
+        t = torch.tensor([1.0 + rank], dtype=torch.float64)   # per-rank elapsed time
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        np.save(os.path.join(out_dir, f"r{rank}.npy"), full.numpy())
+        np.save(os.path.join(out_dir, f"t{rank}.npy"), t.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_predictions_world2(tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    m = CONFIGS["plumbing"]["batch"]
+    expect = torch.cat([_shard_predictions(r) for r in range(world)]).numpy()
+    for r in range(world):
+        got = np.load(tmp_path / f"r{r}.npy")
+        assert got.shape == (world * m, 10)
+        np.testing.assert_array_equal(got, expect)
+        assert float(np.load(tmp_path / f"t{r}.npy")[0]) == float(world)
+
+
+def test_gather_predictions_single_process_is_identity():
+    U = torch.arange(12, dtype=torch.float32).reshape(6, 2)
+    out, work = gather_predictions(U)
+    assert work is None and out is U
+
+
+def test_shards_are_distinct_graphs():
+    a, b = _shard_predictions(0), _shard_predictions(1)
+    assert not torch.equal(a, b)
