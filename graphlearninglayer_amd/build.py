@@ -40,9 +40,9 @@ def _headers_mtime():
     return max(os.path.getmtime(h) for h in hs)
 
 
-def _compile(unit, force, verbose, extra):
+def _compile(unit, force, verbose, extra, objdir=OBJ):
     src = os.path.join(CSRC, unit)
-    obj = os.path.join(OBJ, unit.replace(".hip", ".o"))
+    obj = os.path.join(objdir, unit.replace(".hip", ".o"))
     if (not force and os.path.exists(obj)
             and os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime())):
         return obj
@@ -55,6 +55,24 @@ def _compile(unit, force, verbose, extra):
     if verbose and r.stderr.strip():
         print(r.stderr, file=sys.stderr)
     return obj
+
+
+TRACE_OBJ = os.path.join(OBJ, "trace")
+TRACE_LIB = os.path.join(OBJ, "libgll_trace.so")
+
+
+def build_trace(force=False, verbose=False):
+    """Diagnostic variant with in-kernel timestamps (-DGLL_TRACE): _obj/libgll_trace.so,
+    loaded only by tools/trace_probe.py -- never by the package."""
+    os.makedirs(TRACE_OBJ, exist_ok=True)
+    with cf.ThreadPoolExecutor(len(UNITS)) as ex:
+        objs = list(ex.map(lambda u: _compile(u, force, verbose, ["-DGLL_TRACE"], TRACE_OBJ),
+                           UNITS))
+    cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", TRACE_LIB]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    return TRACE_LIB
 
 
 def build(force=False, verbose=False, extra=()):
@@ -116,7 +134,11 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--resource-usage", action="store_true",
                     help="print per-kernel VGPR/SGPR/LDS/occupancy (-Rpass-analysis)")
+    ap.add_argument("--trace", action="store_true",
+                    help="also build the in-kernel timestamp variant _obj/libgll_trace.so")
     a = ap.parse_args()
+    if a.trace:
+        print(build_trace(force=a.force, verbose=a.verbose))
     extra = ["-Rpass-analysis=kernel-resource-usage"] if a.resource_usage else []
     print(build(force=a.force or a.resource_usage, verbose=a.verbose or a.resource_usage,
                 extra=extra))

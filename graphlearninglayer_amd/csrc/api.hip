@@ -239,3 +239,40 @@ const char* gll_strerror(int code) {
 }
 
 }  // extern "C"
+
+#ifdef GLL_TRACE
+// Diagnostic build only (libgll_trace.so): in-kernel timestamps per translation unit
+// (0 knn, 1 rows, 2 solve, 3 grad), see GLL_TRACE_UNIT in gll_internal.h.
+namespace gll {
+void trace_read_knn(unsigned long long*);
+void trace_read_rows(unsigned long long*);
+void trace_read_solve(unsigned long long*);
+void trace_read_grad(unsigned long long*);
+void trace_reset_knn();
+void trace_reset_rows();
+void trace_reset_solve();
+void trace_reset_grad();
+}  // namespace gll
+
+extern "C" int gll_trace_read(int unit, unsigned long long* out) {
+    (void)hipDeviceSynchronize();
+    switch (unit) {
+        case 0: gll::trace_read_knn(out); return GLL_OK;
+        case 1: gll::trace_read_rows(out); return GLL_OK;
+        case 2: gll::trace_read_solve(out); return GLL_OK;
+        case 3: gll::trace_read_grad(out); return GLL_OK;
+        default: return GLL_ERR_INVALID_ARG;
+    }
+}
+
+extern "C" int gll_trace_reset(int unit) {
+    (void)hipDeviceSynchronize();
+    switch (unit) {
+        case 0: gll::trace_reset_knn(); return GLL_OK;
+        case 1: gll::trace_reset_rows(); return GLL_OK;
+        case 2: gll::trace_reset_solve(); return GLL_OK;
+        case 3: gll::trace_reset_grad(); return GLL_OK;
+        default: return GLL_ERR_INVALID_ARG;
+    }
+}
+#endif

@@ -23,6 +23,53 @@ constexpr int kWave = 64;
 constexpr int kStOvfCount = 8;   // internal status words: overflow-list length
 constexpr int kStBump = 9;       //                        bump-region cursor
 
+// ---------------------------------------------------------------------------------------
+// In-kernel timestamps (diagnostic builds only: build.py --trace defines GLL_TRACE and
+// writes libgll_trace.so; the product library compiles these to nothing).  Per translation
+// unit, 64 words of s_memrealtime (100 MHz): [0,32) checkpoints of block 0 / thread 0,
+// [32,64) (first entry, last exit) pairs of up to 16 kernels over all workgroups.
+// ---------------------------------------------------------------------------------------
+#ifdef GLL_TRACE
+#define GLL_TRACE_UNIT(name)                                                                 \
+    static __device__ unsigned long long g_trace[64];                                       \
+    void trace_read_##name(unsigned long long* out) {                                       \
+        (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), sizeof(g_trace));               \
+    }                                                                                        \
+    void trace_reset_##name() {                                                              \
+        unsigned long long h[64];                                                            \
+        for (int i = 0; i < 64; ++i) h[i] = (i >= 32 && (i & 1) == 0) ? ~0ull : 0ull;       \
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trace), h, sizeof(h));                         \
+    }                                                                                        \
+    struct TraceScope {                                                                      \
+        int k;                                                                               \
+        __device__ explicit TraceScope(int k_) : k(k_) {                                     \
+            if (threadIdx.x == 0) atomicMin(&g_trace[32 + 2 * k], __builtin_amdgcn_s_memrealtime()); \
+        }                                                                                    \
+        __device__ ~TraceScope() {                                                           \
+            if (threadIdx.x == 0) atomicMax(&g_trace[33 + 2 * k], __builtin_amdgcn_s_memrealtime()); \
+        }                                                                                    \
+    };
+#define GLL_TRACE_SCOPE(k) TraceScope gll_trace_scope_(k)
+#define GLL_TRACE_PT(i)                                                                      \
+    do {                                                                                     \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_trace[i] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#define GLL_TRACE_ENTER(k)                                                                   \
+    do {                                                                                     \
+        if (threadIdx.x == 0) atomicMin(&g_trace[32 + 2 * (k)], __builtin_amdgcn_s_memrealtime()); \
+    } while (0)
+#define GLL_TRACE_EXIT(k)                                                                    \
+    do {                                                                                     \
+        if (threadIdx.x == 0) atomicMax(&g_trace[33 + 2 * (k)], __builtin_amdgcn_s_memrealtime()); \
+    } while (0)
+#else
+#define GLL_TRACE_UNIT(name)
+#define GLL_TRACE_SCOPE(k) do {} while (0)
+#define GLL_TRACE_PT(i) do {} while (0)
+#define GLL_TRACE_ENTER(k) do {} while (0)
+#define GLL_TRACE_EXIT(k) do {} while (0)
+#endif
+
 struct Layout {
     int n, d, base, m, C, K;
     int ldD;          // leading dimension of the n x n squared-distance matrix

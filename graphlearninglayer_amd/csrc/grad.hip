@@ -16,6 +16,8 @@
 
 namespace gll {
 
+GLL_TRACE_UNIT(grad)
+
 struct EdgeArgs {
     int n, base, C, K, d;
     const int32_t* row_start;
@@ -47,6 +49,7 @@ __device__ __forceinline__ float edge_gv(const EdgeArgs& a, int i, int j, float 
 
 // auto eps, pass 1: S_ij and b_i
 __global__ __launch_bounds__(256) void edge_coef_kernel(EdgeArgs a) {
+    GLL_TRACE_SCOPE(0);
     const int lane = lane_id();
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
@@ -67,6 +70,7 @@ __global__ __launch_bounds__(256) void edge_coef_kernel(EdgeArgs a) {
 template <bool AUTO, int ND, bool VEC>
 __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float* __restrict__ X,
                                                         float* __restrict__ out) {
+    GLL_TRACE_SCOPE(1);
     const int lane = lane_id();
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;

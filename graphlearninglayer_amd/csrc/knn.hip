@@ -23,6 +23,8 @@
 
 namespace gll {
 
+GLL_TRACE_UNIT(knn)
+
 // --------------------------------------------------------------------------------------
 // K1a: symmetric Gram tile.  D2 is symmetric, so only tiles bi <= bj are computed and the
 // off-diagonal ones are written twice (D2[i][j] and D2[j][i] bitwise equal).  512 threads:
@@ -58,6 +60,7 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
                                                        int T, float* __restrict__ D2, int ld,
                                                        int32_t* __restrict__ status,
                                                        int32_t* __restrict__ rev_cnt) {
+    GLL_TRACE_SCOPE(0);
     // stage[buf][half][A|B][64 rows][kGLD] ; the epilogue reuses the same storage
     __shared__ __attribute__((aligned(16))) float smem[2 * 2 * 2 * 64 * kGLD];
     __shared__ float s_sq[2][64];
@@ -294,6 +297,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ rev_cnt,
     int32_t* __restrict__ rev_idx, float* __restrict__ rev_d2, int32_t* __restrict__ ovf,
     int32_t* __restrict__ status, int32_t* __restrict__ status_pub) {
+    GLL_TRACE_SCOPE(1);
     const int lane = lane_id();
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;  // whole wave

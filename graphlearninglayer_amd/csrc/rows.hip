@@ -17,6 +17,8 @@
 
 namespace gll {
 
+GLL_TRACE_UNIT(rows)
+
 constexpr int kStage = 256;      // per-wave LDS staging capacity (entries)
 constexpr int kMaxCPerLane = 4;  // classes per lane in the rhs accumulation (C <= 256)
 
@@ -183,6 +185,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
 
 template <typename TY>
 __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __restrict__ Y) {
+    GLL_TRACE_SCOPE(0);
     __shared__ int s_col[4][kStage];
     __shared__ float s_d2[4][kStage];
     __shared__ int t_col[4][kStage];

@@ -27,6 +27,8 @@
 
 namespace gll {
 
+GLL_TRACE_UNIT(solve)
+
 static constexpr size_t kLdsLimit = 160 * 1024;
 
 // Opt a kernel into the full 160 KiB of dynamic LDS, once per kernel (host-side cost).
@@ -114,6 +116,8 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     float x[R], r[R], p[R], ap[R], mi[R], dg[R];
     float rz = 0.f, bb = 0.f;
     int tov = 0;
+    GLL_TRACE_SCOPE(0);
+    GLL_TRACE_PT(0);
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int u = tid + NT * q;
@@ -146,6 +150,7 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
             bb += r[q] * r[q];
         }
     }
+    GLL_TRACE_PT(1);
     // entries beyond the ELL slices: compact them into LDS when they fit
     int ov_total = 0;
     int ooff = block_excl_scan<NT>(tov, scan, ov_total);
@@ -164,9 +169,11 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
             }
         }
     }
+    GLL_TRACE_PT(2);
     int phase = 0;
     if constexpr (NT > kWave) __syncthreads();
     block_sum2<NT>(rz, bb, red, phase);
+    GLL_TRACE_PT(3);
     const float tol2 = rtol * rtol * bb;
     int it = 0;
     bool conv = !(bb > 0.f);
@@ -193,7 +200,9 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
             ap[q] = dg[q] * p[q] - acc;   // (Luu p)_u = (deg_u + tau) p_u - sum_j W_uj p_j
             pap += p[q] * ap[q];
         }
+        if (it == 1) GLL_TRACE_PT(4);
         block_sum2<NT>(pap, unused, red, phase);
+        if (it == 1) GLL_TRACE_PT(5);
         if (!(pap > 0.f)) break;   // breakdown or NaN: stop, reported as non-converged
         const float alpha = rz / pap;
         float rr = 0.f, rzn = 0.f;
@@ -205,6 +214,7 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
             rzn += r[q] * mi[q] * r[q];
         }
         block_sum2<NT>(rr, rzn, red, phase);
+        if (it == 1) GLL_TRACE_PT(6);
         if (rr <= tol2) {
             conv = true;
             break;
@@ -218,7 +228,9 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
             if (u < m) P_[u] = p[q];
         }
         if constexpr (NT > kWave) __syncthreads();
+        if (it == 1) GLL_TRACE_PT(7);
     }
+    GLL_TRACE_PT(8);
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int u = tid + NT * q;
@@ -231,6 +243,7 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
         if (st_iters) atomicMax(st_iters, it);
         if (!conv && st_nonconv) atomicAdd(st_nonconv, 1);
     }
+    GLL_TRACE_PT(9);
 }
 
 // Large systems: vectors in LDS (<= 160 KiB) or in the workspace.

@@ -1,0 +1,101 @@
+"""In-kernel timeline of one NS fwd+bwd call (diagnostic, GPU box).
+
+Loads the timestamp build (_obj/libgll_trace.so, `python -m graphlearninglayer_amd.build
+--trace`), runs forward then backward at the NS config through the C ABI and prints, per
+kernel, first-workgroup entry -> last-workgroup exit, the gaps between consecutive kernels,
+and the block-0 checkpoints of the CG kernel.  Clock: s_memrealtime, 100 MHz.
+"""
+import ctypes as ct
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from graphlearninglayer_amd import GLL, _lib  # noqa: E402
+from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth  # noqa: E402
+
+TICK_US = 0.01
+lib = ct.CDLL(os.path.join(ROOT, "graphlearninglayer_amd", "_obj", "libgll_trace.so"))
+lib.gll_workspace_bytes.restype = ct.c_size_t
+lib.gll_trace_read.argtypes = [ct.c_int, ct.POINTER(ct.c_ulonglong)]
+UNITS = {0: ("knn", ["gram", "select"]), 1: ("rows", ["row_build"]),
+         2: ("solve", ["cg_ell", "cg_lds", "cg_csr"]), 3: ("grad", ["edge_coef", "grad_spmm"])}
+CG_PTS = ["entry", "ell loaded+P", "ovf compacted", "rz/bb reduced", "it1 spmv", "it1 pAp",
+          "it1 rr", "it1 P published", "loop done", "stored"]
+
+cfg_name = os.environ.get("TRACE_CFG", "ns")
+c = CONFIGS[cfg_name]
+n, base, d, k = c["base"] + c["batch"], c["base"], c["d"], c["k"]
+eps = float(os.environ.get("TRACE_EPS", "1.0"))
+dev = torch.device("cuda", 0)
+X_np, lab = synth(base, n - base, d, r=c["r"], seed=0)
+X = torch.from_numpy(X_np).to(dev)
+Y = torch.from_numpy(one_hot(lab[:base])).to(dev)
+g = torch.from_numpy(seeded_gbar(n - base, 10)).to(dev)
+prob = GLL.make_problem(n, d, base, 10, k, 0.07, eps)
+ws = torch.empty(lib.gll_workspace_bytes(ct.byref(prob)), dtype=torch.uint8, device=dev)
+U = torch.empty(n - base, 10, dtype=torch.float64, device=dev)
+gx = torch.empty(n, d, dtype=torch.float32, device=dev)
+s = ct.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def fwd():
+    assert lib.gll_forward(ct.byref(prob), ct.c_void_p(X.data_ptr()), ct.c_void_p(Y.data_ptr()), 0,
+                           ct.c_void_p(ws.data_ptr()), ct.c_void_p(U.data_ptr()), s) == 0
+
+
+def bwd():
+    assert lib.gll_backward(ct.byref(prob), ct.c_void_p(X.data_ptr()), ct.c_void_p(Y.data_ptr()), 0,
+                            ct.c_void_p(ws.data_ptr()), ct.c_void_p(g.data_ptr()), 1,
+                            ct.c_void_p(gx.data_ptr()), s) == 0
+
+
+def read_all():
+    out = {}
+    for u in UNITS:
+        buf = (ct.c_ulonglong * 64)()
+        lib.gll_trace_read(u, buf)
+        out[u] = np.array(buf[:], dtype=np.uint64)
+    return out
+
+
+def timeline(tr, label):
+    spans = []
+    for u, (_, kns) in UNITS.items():
+        for i, kn in enumerate(kns):
+            a, b = int(tr[u][32 + 2 * i]), int(tr[u][33 + 2 * i])
+            if a != 2 ** 64 - 1 and b != 0:
+                spans.append((a, b, kn))
+    spans.sort()
+    t0 = spans[0][0]
+    print(f"--- {label} (us from first entry)")
+    prev = None
+    for a, b, kn in spans:
+        gap = "" if prev is None else f"  gap {TICK_US * (a - prev):6.2f}"
+        print(f"{kn:10s} {TICK_US * (a - t0):7.2f} -> {TICK_US * (b - t0):7.2f}  "
+              f"({TICK_US * (b - a):6.2f}){gap}")
+        prev = b
+    pts = tr[2][:10].astype(np.int64)
+    if pts[0]:
+        print("cg block 0: " + ", ".join(f"{CG_PTS[i]} +{TICK_US * (pts[i] - pts[0]):.2f}"
+                                         for i in range(1, 10) if pts[i]))
+
+
+for _ in range(10):
+    fwd()
+    bwd()
+torch.cuda.synchronize()
+for rep in range(3):
+    for u in UNITS:
+        lib.gll_trace_reset(u)
+    fwd()
+    torch.cuda.synchronize()
+    timeline(read_all(), f"forward rep {rep}")
+    for u in UNITS:
+        lib.gll_trace_reset(u)
+    bwd()
+    torch.cuda.synchronize()
+    timeline(read_all(), f"backward rep {rep}")
