@@ -248,6 +248,8 @@ void trace_read_knn(unsigned long long*);
 void trace_read_rows(unsigned long long*);
 void trace_read_solve(unsigned long long*);
 void trace_read_grad(unsigned long long*);
+void trace_read_wg_knn(unsigned long long*);
+void trace_read_wg_solve(unsigned long long*);
 void trace_reset_knn();
 void trace_reset_rows();
 void trace_reset_solve();
@@ -261,6 +263,15 @@ extern "C" int gll_trace_read(int unit, unsigned long long* out) {
         case 1: gll::trace_read_rows(out); return GLL_OK;
         case 2: gll::trace_read_solve(out); return GLL_OK;
         case 3: gll::trace_read_grad(out); return GLL_OK;
+        default: return GLL_ERR_INVALID_ARG;
+    }
+}
+
+extern "C" int gll_trace_read_wg(int unit, unsigned long long* out) {
+    (void)hipDeviceSynchronize();
+    switch (unit) {
+        case 0: gll::trace_read_wg_knn(out); return GLL_OK;
+        case 2: gll::trace_read_wg_solve(out); return GLL_OK;
         default: return GLL_ERR_INVALID_ARG;
     }
 }

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "gll.h"
 
@@ -26,14 +27,19 @@ constexpr int kStBump = 9;       //                        bump-region cursor
 // ---------------------------------------------------------------------------------------
 // In-kernel timestamps (diagnostic builds only: build.py --trace defines GLL_TRACE and
 // writes libgll_trace.so; the product library compiles these to nothing).  Per translation
-// unit, 64 words of s_memrealtime (100 MHz): [0,32) checkpoints of block 0 / thread 0,
-// [32,64) (first entry, last exit) pairs of up to 16 kernels over all workgroups.
+// unit, 64 words of s_memrealtime (100 MHz): [0,24) checkpoints of block 0 / thread 0,
+// [24,32) last workgroup entry of kernel k < 8, [32,64) (first entry, last exit) pairs of up
+// to 16 kernels over all workgroups.
 // ---------------------------------------------------------------------------------------
 #ifdef GLL_TRACE
 #define GLL_TRACE_UNIT(name)                                                                 \
     static __device__ unsigned long long g_trace[64];                                       \
+    static __device__ unsigned long long g_wg[3 * 4096]; /* kernel 0: entry, exit, cu id */ \
     void trace_read_##name(unsigned long long* out) {                                       \
         (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), sizeof(g_trace));               \
+    }                                                                                        \
+    void trace_read_wg_##name(unsigned long long* out) {                                    \
+        (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg), sizeof(g_wg));                     \
     }                                                                                        \
     void trace_reset_##name() {                                                              \
         unsigned long long h[64];                                                            \
@@ -43,10 +49,22 @@ constexpr int kStBump = 9;       //                        bump-region cursor
     struct TraceScope {                                                                      \
         int k;                                                                               \
         __device__ explicit TraceScope(int k_) : k(k_) {                                     \
-            if (threadIdx.x == 0) atomicMin(&g_trace[32 + 2 * k], __builtin_amdgcn_s_memrealtime()); \
+            if (threadIdx.x == 0) {                                                          \
+                const unsigned long long t = __builtin_amdgcn_s_memrealtime();               \
+                atomicMin(&g_trace[32 + 2 * k], t);                                          \
+                atomicMax(&g_trace[24 + k], t);                                              \
+                if (k == 0 && blockIdx.x < 4096) {                                           \
+                    g_wg[blockIdx.x] = t;                                                    \
+                    g_wg[2 * 4096 + blockIdx.x] = __smid();                                  \
+                }                                                                            \
+            }                                                                                \
         }                                                                                    \
         __device__ ~TraceScope() {                                                           \
-            if (threadIdx.x == 0) atomicMax(&g_trace[33 + 2 * k], __builtin_amdgcn_s_memrealtime()); \
+            if (threadIdx.x == 0) {                                                          \
+                const unsigned long long t = __builtin_amdgcn_s_memrealtime();               \
+                atomicMax(&g_trace[33 + 2 * k], t);                                          \
+                if (k == 0 && blockIdx.x < 4096) g_wg[4096 + blockIdx.x] = t;                \
+            }                                                                                \
         }                                                                                    \
     };
 #define GLL_TRACE_SCOPE(k) TraceScope gll_trace_scope_(k)
@@ -70,8 +88,25 @@ constexpr int kStBump = 9;       //                        bump-region cursor
 #define GLL_TRACE_EXIT(k) do {} while (0)
 #endif
 
+// Split of the Gram contraction over workgroups: each of KS workgroups of a 64x64 tile takes
+// a contiguous slice of the features and writes its own partial plane of D2; the select
+// kernel sums the planes in a fixed order.  Measured on MI355X at NS (tools/dispatch_probe.py,
+// profiles/r01_gram_dispatch.txt): a tile runs ~2 us per 64-deep chunk on one CU
+// (MFMA-bound), and KS = 2 / 4 overflow the 256 CUs into extra rounds (21.5 / 23.5 us against
+// 16.9 us for KS = 1), so even splits never pay; KS stays 1 until a balanced (stream-K)
+// schedule replaces them.
+inline int gram_splits(int n, int d) {
+#ifdef GLL_TRACE
+    if (const char* e = getenv("GLL_GRAM_KS")) return atoi(e);   // diagnostic sweeps only
+#endif
+    (void)n;
+    (void)d;
+    return 1;
+}
+
 struct Layout {
     int n, d, base, m, C, K;
+    int KS;           // Gram split planes (gram_splits)
     int ldD;          // leading dimension of the n x n squared-distance matrix
     int RCAP;         // reverse-list capacity per row
     int Wcap;         // slot width of a row
@@ -84,6 +119,7 @@ struct Layout {
         K = p.K < p.n ? p.K : p.n;
         m = n - base;
         ldD = (n + 3) & ~3;
+        KS = gram_splits(n, d);
         RCAP = 4 * (K - 1) + 8;
         Wcap = (K - 1) + RCAP;
         Etot = int64_t(n) * Wcap + 2LL * n * (K - 1);
@@ -94,7 +130,7 @@ struct Layout {
             return at;
         };
         status = take(GLL_ST_NWORDS * 4);
-        D2 = take(size_t(n) * ldD * 4);
+        D2 = take(size_t(KS) * n * ldD * 4);   // KS partial planes
         knn_idx = take(size_t(n) * K * 4);
         knn_d2 = take(size_t(n) * K * 4);
         eps = take(size_t(n) * 4);
@@ -236,6 +272,35 @@ __device__ __forceinline__ f32x4 load4(const float* __restrict__ p, int k, int l
         v.w = k + 3 < lim ? e : 0.f;
     }
     return v;
+}
+
+// load4 split in two halves for software pipelining: the load (address clamped into the
+// row, never branched) and the zero-mask of the lanes past `lim`, applied where the value
+// is consumed -- a mask right after the load would make the wave wait for it there.
+template <bool VEC>
+__device__ __forceinline__ f32x4 load4_raw(const float* __restrict__ p, int k, int lim) {
+    f32x4 v;
+    if constexpr (VEC) {
+        v = *reinterpret_cast<const f32x4*>(p + (k < lim ? k : 0));
+    } else {
+        v.x = p[k + 0 < lim ? k + 0 : 0];
+        v.y = p[k + 1 < lim ? k + 1 : 0];
+        v.z = p[k + 2 < lim ? k + 2 : 0];
+        v.w = p[k + 3 < lim ? k + 3 : 0];
+    }
+    return v;
+}
+template <bool VEC>
+__device__ __forceinline__ f32x4 mask4(f32x4 v, int k, int lim) {
+    if constexpr (VEC) {
+        return k < lim ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+        v.x = k + 0 < lim ? v.x : 0.f;
+        v.y = k + 1 < lim ? v.y : 0.f;
+        v.z = k + 2 < lim ? v.z : 0.f;
+        v.w = k + 3 < lim ? v.w : 0.f;
+        return v;
+    }
 }
 
 // ---------------------------------------------------------------------------------------

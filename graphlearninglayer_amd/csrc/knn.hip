@@ -19,6 +19,8 @@
 //                          built without an n x n structure or a prefix sum.
 #include <limits.h>
 
+#include <type_traits>
+
 #include "gll_internal.h"
 
 namespace gll {
@@ -27,12 +29,21 @@ GLL_TRACE_UNIT(knn)
 
 // --------------------------------------------------------------------------------------
 // K1a: symmetric Gram tile.  D2 is symmetric, so only tiles bi <= bj are computed and the
-// off-diagonal ones are written twice (D2[i][j] and D2[j][i] bitwise equal).  512 threads:
-// waves 0-3 and 4-7 split the feature dimension in halves (split-K inside the workgroup,
-// combined through LDS in a fixed order), each wave a 32x32 quadrant of the 64x64 tile.
-// The finished tile is staged in LDS so both orientations leave as coalesced row stores.
+// off-diagonal ones are written in both orientations.  Small problems have fewer tiles than
+// CUs, so the feature dimension is split over KS workgroups per tile (gram_splits): each
+// writes a partial plane  |a_i|^2_s + |b_j|^2_s - 2 <a_i, b_j>_s  over its slice s, and the
+// select kernel adds the planes in a fixed order -- no inter-workgroup synchronisation.
+//
+// 512 threads = 8 waves: wave (kh, qd) owns the 32x32 quadrant qd of the 64x64 tile and the
+// k-half kh of every 64-deep chunk (split-K inside the workgroup, halves combined in LDS in a
+// fixed order).  Operands stream through a register ring of NCH chunks: chunk c of the next
+// super-chunk is loaded into ring slot c right after slot c went to LDS, so a load has
+// NCH-1 chunks of MFMA work to hide behind; LDS is double-buffered per chunk.
 // --------------------------------------------------------------------------------------
-// 16 MFMAs over one 32-k chunk: lane (r, h) holds A[r][8u + 4h + t], B[c=r][8u + 4h + t]
+constexpr int kGK = 64;         // k per LDS chunk
+constexpr int kGL = kGK + 4;    // padded LDS row (floats): conflict-free ds_read_b128
+
+// 16 MFMAs over 32 k: lane (r, h) holds A[r][8u + 4h + t], B[c=r][8u + 4h + t]
 __device__ __forceinline__ void gram_chunk_mfma(const f32x4 (&a)[4], const f32x4 (&b)[4],
                                                 f32x16& acc, float& sa, float& sb) {
 #pragma unroll
@@ -46,31 +57,25 @@ __device__ __forceinline__ void gram_chunk_mfma(const f32x4 (&a)[4], const f32x4
     }
 }
 
-// --------------------------------------------------------------------------------------
-// Every 32-wide k-chunk of the tile's 64 A rows and 64 B rows is fetched once per
-// workgroup with coalesced 16-B loads (8 lanes per 128-B row segment), staged in padded LDS
-// rows (36 floats: conflict-free ds_read_b128 for the MFMA fragments) and double-buffered:
-// chunk c+1 is in registers on its way to LDS while chunk c feeds the MFMAs.
-// --------------------------------------------------------------------------------------
-constexpr int kGBK = 32;        // k per chunk
-constexpr int kGLD = kGBK + 4;  // padded LDS row (floats)
-
-template <bool VEC>
+template <bool VEC, int NCH>
 __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__ X, int n, int d,
-                                                       int T, float* __restrict__ D2, int ld,
+                                                       int T, int KS, int kspan,
+                                                       float* __restrict__ D2, int ld,
+                                                       size_t plane,
                                                        int32_t* __restrict__ status,
                                                        int32_t* __restrict__ rev_cnt) {
     GLL_TRACE_SCOPE(0);
-    // stage[buf][half][A|B][64 rows][kGLD] ; the epilogue reuses the same storage
-    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * 2 * 64 * kGLD];
+    // stage[buf][A|B][64 rows][kGL]; the epilogue reuses the same storage
+    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * 64 * kGL];
     __shared__ float s_sq[2][64];
     const int tid = threadIdx.x;
     const int lane = lane_id();
     const int wave = tid >> 6;
-    const int kh = wave >> 2;             // feature half of this wave
+    const int kh = wave >> 2;             // k-half of every chunk
     const int qd = wave & 3;              // 32x32 quadrant of this wave
     const int r = lane & 31, h = lane >> 5;
-    int bi = 0, rem = blockIdx.x;
+    const int ks = blockIdx.x % KS;
+    int bi = 0, rem = blockIdx.x / KS;
     while (rem >= T - bi) {
         rem -= T - bi;
         ++bi;
@@ -81,62 +86,73 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
         if (g < GLL_ST_NWORDS) status[g] = 0;
         for (int q = g; q < n; q += gridDim.x * 512) rev_cnt[q] = 0;
     }
-    const int dh = ((d + 2 * kGBK - 1) / (2 * kGBK)) * kGBK;   // per-half span, x32
-    const int nchunk = dh / kGBK;                                // same for both halves
-    // loader role: the 256 threads of half `kh` load that half's chunks.  Thread t loads
-    // rows (t >> 3) and (t >> 3) + 32 of A and B at column 4 (t & 7).
-    const int lt = tid & 255;
-    const int lrow = lt >> 3, lcol = 4 * (lt & 7);
-    const int k_lo = kh * dh;
-    const int k_hi = min(d, k_lo + dh);
+    GLL_TRACE_PT(10);
+    const int k_lo = ks * kspan;
+    const int k_hi = min(d, k_lo + kspan);
+    const int nsup = kspan / (kGK * NCH);
+    // loader role: thread t moves float4 column 4 (t & 15) of rows (t >> 4) and (t >> 4) + 32
+    // of A and of B for every chunk
+    const int lrow = tid >> 4, lcol = 4 * (tid & 15);
     const float* ga0 = X + size_t(min(bi * 64 + lrow, n - 1)) * d;
     const float* ga1 = X + size_t(min(bi * 64 + lrow + 32, n - 1)) * d;
     const float* gb0 = X + size_t(min(bj * 64 + lrow, n - 1)) * d;
     const float* gb1 = X + size_t(min(bj * 64 + lrow + 32, n - 1)) * d;
-    auto stage = [&](int buf, int which) -> float* {
-        return smem + ((buf * 2 + kh) * 2 + which) * 64 * kGLD;
+    f32x4 ring[NCH][4];
+    auto gload = [&](int chunk, f32x4 (&v)[4]) {   // raw: masked when stored to LDS
+        const int k = k_lo + chunk * kGK + lcol;
+        v[0] = load4_raw<VEC>(ga0, k, k_hi);
+        v[1] = load4_raw<VEC>(ga1, k, k_hi);
+        v[2] = load4_raw<VEC>(gb0, k, k_hi);
+        v[3] = load4_raw<VEC>(gb1, k, k_hi);
     };
-    f32x4 la0, la1, lb0, lb1;
-    auto gload = [&](int c) {
-        const int k = k_lo + c * kGBK + lcol;
-        la0 = load4<VEC>(ga0, k, k_hi);
-        la1 = load4<VEC>(ga1, k, k_hi);
-        lb0 = load4<VEC>(gb0, k, k_hi);
-        lb1 = load4<VEC>(gb1, k, k_hi);
-    };
-    auto lstore = [&](int buf) {
-        float* A = stage(buf, 0);
-        float* B = stage(buf, 1);
-        *reinterpret_cast<f32x4*>(A + lrow * kGLD + lcol) = la0;
-        *reinterpret_cast<f32x4*>(A + (lrow + 32) * kGLD + lcol) = la1;
-        *reinterpret_cast<f32x4*>(B + lrow * kGLD + lcol) = lb0;
-        *reinterpret_cast<f32x4*>(B + (lrow + 32) * kGLD + lcol) = lb1;
+    auto lstore = [&](int chunk, int buf, const f32x4 (&v)[4]) {
+        const int k = k_lo + chunk * kGK + lcol;
+        float* A = smem + (buf * 2 + 0) * 64 * kGL;
+        float* B = smem + (buf * 2 + 1) * 64 * kGL;
+        *reinterpret_cast<f32x4*>(A + lrow * kGL + lcol) = mask4<VEC>(v[0], k, k_hi);
+        *reinterpret_cast<f32x4*>(A + (lrow + 32) * kGL + lcol) = mask4<VEC>(v[1], k, k_hi);
+        *reinterpret_cast<f32x4*>(B + lrow * kGL + lcol) = mask4<VEC>(v[2], k, k_hi);
+        *reinterpret_cast<f32x4*>(B + (lrow + 32) * kGL + lcol) = mask4<VEC>(v[3], k, k_hi);
     };
     f32x16 acc;
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = 0.f;
     float sa = 0.f, sb = 0.f;
     const int arow = (qd >> 1) * 32 + r, brow = (qd & 1) * 32 + r;
-    gload(0);
-    lstore(0);
-    if (nchunk > 1) gload(1);
-    __syncthreads();
-    for (int c = 0; c < nchunk; ++c) {
-        const int buf = c & 1;
-        const float* A = stage(buf, 0) + arow * kGLD + 4 * h;
-        const float* B = stage(buf, 1) + brow * kGLD + 4 * h;
-        f32x4 a[4], b[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            a[u] = *reinterpret_cast<const f32x4*>(A + 8 * u);
-            b[u] = *reinterpret_cast<const f32x4*>(B + 8 * u);
+    for (int c = 0; c < NCH; ++c) gload(c, ring[c]);
+    // one super-chunk: chunks straight from the ring.  Several: ring slot c is reloaded with
+    // the next super-chunk's chunk c right after it went to LDS -- unconditionally (the last
+    // super-chunk re-reads its own, clamped), so the outstanding-load count is the same on
+    // every path and the compiler waits for exactly the slot it stores next.
+    auto run_super = [&](int sc, auto reload) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int buf = (sc * NCH + c) & 1;
+            lstore(sc * NCH + c, buf, ring[c]);
+            if constexpr (decltype(reload)::value) gload(min(sc + 1, nsup - 1) * NCH + c, ring[c]);
+            __syncthreads();
+            if (sc == 0 && c == 0) GLL_TRACE_PT(15);
+            const float* A = smem + (buf * 2 + 0) * 64 * kGL + arow * kGL + kh * 32 + 4 * h;
+            const float* B = smem + (buf * 2 + 1) * 64 * kGL + brow * kGL + kh * 32 + 4 * h;
+            f32x4 a[4], b[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                a[u] = *reinterpret_cast<const f32x4*>(A + 8 * u);
+                b[u] = *reinterpret_cast<const f32x4*>(B + 8 * u);
+            }
+            gram_chunk_mfma(a, b, acc, sa, sb);
         }
-        if (c + 1 < nchunk) lstore(buf ^ 1);   // chunk c+1: registers -> LDS (other buffer)
-        if (c + 2 < nchunk) gload(c + 2);      // chunk c+2: HBM/L2 -> registers
-        gram_chunk_mfma(a, b, acc, sa, sb);
-        __syncthreads();
+    };
+    if (nsup == 1) {
+        run_super(0, std::false_type{});
+        GLL_TRACE_PT(11);
+    } else {
+        for (int sc = 0; sc < nsup; ++sc) run_super(sc, std::true_type{});
     }
-    // combine the feature halves in a fixed order (half 0 + half 1) through LDS
+    __syncthreads();
+    GLL_TRACE_PT(12);
+    // combine the k-halves in a fixed order (half 0 + half 1) through LDS
     float* part = smem;                    // [4 quadrants][16][64]
     float* nrm = smem + 4 * 16 * 64;       // [2][4][64]
     if (kh == 1) {
@@ -170,21 +186,24 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
         }
     }
     __syncthreads();
+    GLL_TRACE_PT(13);
+    float* P = D2 + size_t(ks) * plane;
     const int cr = tid >> 4, cc = (tid & 15) * 4;
     for (int rr = cr; rr < 64; rr += 32) {
         const int i = bi * 64 + rr;
         if (i < n) {
 #pragma unroll
             for (int t = 0; t < 4; ++t)
-                if (bj * 64 + cc + t < n) D2[size_t(i) * ld + bj * 64 + cc + t] = tile[rr * 65 + cc + t];
+                if (bj * 64 + cc + t < n) P[size_t(i) * ld + bj * 64 + cc + t] = tile[rr * 65 + cc + t];
         }
         const int jr = bj * 64 + rr;
         if (bi != bj && jr < n) {
 #pragma unroll
             for (int t = 0; t < 4; ++t)
-                if (bi * 64 + cc + t < n) D2[size_t(jr) * ld + bi * 64 + cc + t] = tile[(cc + t) * 65 + rr];
+                if (bi * 64 + cc + t < n) P[size_t(jr) * ld + bi * 64 + cc + t] = tile[(cc + t) * 65 + rr];
         }
     }
+    GLL_TRACE_PT(14);
 }
 
 // --------------------------------------------------------------------------------------
@@ -213,24 +232,39 @@ __device__ __forceinline__ void list_pop(uint64_t (&key)[KC], bool pop) {
     key[KC - 1] = pop ? ~0ull : key[KC - 1];
 }
 
-// Per-lane scan of row i of D2 into a sorted list of the lane's KC smallest keys; returns
-// how many valid columns the lane saw.
-template <int KC>
-__device__ __forceinline__ int scan_row(const float* __restrict__ row, int n, int i,
-                                        uint64_t (&key)[KC]) {
+// Per-lane scan of row i of D2 (the sum of NP partial planes, added in plane order) into a
+// sorted list of the lane's KC smallest keys; returns how many valid columns the lane saw.
+// NB float4 per lane and plane are loaded before any is consumed (one memory latency per
+// 256*NB columns); addresses past the row are clamped, not branched around.
+template <int KC, int NP>
+__device__ __forceinline__ int scan_row(const float* __restrict__ row, size_t plane, int n,
+                                        int ld, int i, uint64_t (&key)[KC]) {
+    constexpr int NB = 4;
     const int lane = lane_id();
 #pragma unroll
     for (int t = 0; t < KC; ++t) key[t] = ~0ull;
     int seen = 0;
-    for (int j0 = 4 * lane; j0 < n; j0 += 4 * kWave) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(row + j0);
+    for (int jb = 0; jb < n; jb += 4 * kWave * NB) {
+        f32x4 v[NB];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int j = j0 + t;
-            if (j < n && j != i && v[t] == v[t]) {   // NaN rows never enter
-                ++seen;
-                const uint64_t kv = pack_key(v[t], j);
-                if (kv < key[KC - 1]) list_insert<KC>(key, kv);
+        for (int b = 0; b < NB; ++b) {
+            const int j0 = jb + 4 * (b * kWave + lane);
+            const int jc = j0 < ld ? j0 : 0;
+            v[b] = *reinterpret_cast<const f32x4*>(row + jc);
+#pragma unroll
+            for (int p = 1; p < NP; ++p) v[b] += *reinterpret_cast<const f32x4*>(row + p * plane + jc);
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int j0 = jb + 4 * (b * kWave + lane);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int j = j0 + t;
+                if (j < n && j != i && v[b][t] == v[b][t]) {   // NaN rows never enter
+                    ++seen;
+                    const uint64_t kv = pack_key(v[b][t], j);
+                    if (kv < key[KC - 1]) list_insert<KC>(key, kv);
+                }
             }
         }
     }
@@ -290,9 +324,9 @@ __device__ __forceinline__ bool merge_fast(uint64_t (&key)[KS], int kc, int seen
     return __ballot(popped == KS && seen > KS) != 0;
 }
 
-template <int KC, bool VEC>
+template <int KC, bool VEC, int NP>
 __global__ __launch_bounds__(256) void knn_select_kernel(
-    const float* __restrict__ D2, int ld, const float* __restrict__ X, int n, int d, int K,
+    const float* __restrict__ D2, int ld, size_t plane, const float* __restrict__ X, int n, int d, int K,
     int kc, float eps_fixed, int auto_eps, int RCAP, int32_t* __restrict__ knn_idx,
     float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ rev_cnt,
     int32_t* __restrict__ rev_idx, float* __restrict__ rev_d2, int32_t* __restrict__ ovf,
@@ -308,11 +342,13 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     int ci;
     {
         uint64_t key[KS];
-        const int seen = scan_row<KS>(row, n, i, key);
+        const int seen = scan_row<KS, NP>(row, plane, n, ld, i, key);
+        GLL_TRACE_PT(16);
         const bool redo = merge_fast<KS>(key, kc, seen, ci);
+        GLL_TRACE_PT(17);
         if (redo) {
             uint64_t full[KC];
-            scan_row<KC>(row, n, i, full);
+            scan_row<KC, NP>(row, plane, n, ld, i, full);
             ci = merge_exact<KC>(full, kc);
         }
     }
@@ -325,15 +361,23 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
         const bool live = p0 + grp < kc && j >= 0;
         const float* xj = X + size_t(live ? j : i) * d;
         float part = 0.f;
-#pragma unroll 4
-        for (int k = 4 * sub; k < d; k += 32) {
-            const f32x4 a = load4<VEC>(xi, k, d);
-            const f32x4 bb = load4<VEC>(xj, k, d);
-            const f32x4 df = a - bb;
-            part += df.x * df.x;
-            part += df.y * df.y;
-            part += df.z * df.z;
-            part += df.w * df.w;
+        for (int kb = 0; kb < d; kb += 512) {   // 16 steps of 32 features: all loads in flight
+            f32x4 va[16], vb[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {   // straight-line: every load issued before use
+                const int k = kb + 32 * u + 4 * sub;
+                va[u] = load4_raw<VEC>(xi, k, d);
+                vb[u] = load4_raw<VEC>(xj, k, d);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int k = kb + 32 * u + 4 * sub;
+                const f32x4 df = mask4<VEC>(va[u] - vb[u], k, d);
+                part += df.x * df.x;
+                part += df.y * df.y;
+                part += df.z * df.z;
+                part += df.w * df.w;
+            }
         }
         part = group8_sum(part);
 #pragma unroll
@@ -342,6 +386,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
             if (lane == p0 + g) ce = v;
         }
     }
+    GLL_TRACE_PT(18);
     if (ci < 0) ce = __builtin_inff();
     // 4) rank the candidates by (exact d^2, index); keep the K-1 nearest
     const uint64_t myk = ci < 0 ? ~0ull : pack_key(ce, ci);
@@ -370,6 +415,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
         oi[1 + lane] = i;
         od[1 + lane] = 0.f;
     }
+    GLL_TRACE_PT(19);
     float ei = eps_fixed;
     if (auto_eps) {
         // eps_i = d(i, knn_ind[i, K-1])  (GLL.py:205)
@@ -398,12 +444,25 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
 hipError_t launch_gram(const Layout& L, void* ws, const float* X, bool vec, hipStream_t s) {
     const int T = (L.n + 63) / 64;
     const int tiles = T * (T + 1) / 2;
+    const int KS = L.KS;
+    // slice of the features per split, in whole 64-deep chunks, grouped NCH per super-chunk
+    int kspan = ((L.d + KS - 1) / KS + kGK - 1) / kGK * kGK;
+    const int NCH = kspan >= 4 * kGK ? 4 : (kspan >= 2 * kGK ? 2 : 1);
+    kspan = (kspan + NCH * kGK - 1) / (NCH * kGK) * (NCH * kGK);
     float* D2 = L.at<float>(ws, L.D2);
+    const size_t plane = size_t(L.n) * L.ldD;
     int32_t* st = L.at<int32_t>(ws, L.status);
     int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
+    const dim3 grid(tiles * KS);
     prof_begin(GLL_K_GRAM, s);
-    if (vec) gram_lds_kernel<true><<<tiles, 512, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc);
-    else gram_lds_kernel<false><<<tiles, 512, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc);
+#define GLL_GRAM(V, N) \
+    gram_lds_kernel<V, N><<<grid, 512, 0, s>>>(X, L.n, L.d, T, KS, kspan, D2, L.ldD, plane, st, rc)
+    if (vec) {
+        if (NCH == 4) GLL_GRAM(true, 4); else if (NCH == 2) GLL_GRAM(true, 2); else GLL_GRAM(true, 1);
+    } else {
+        if (NCH == 4) GLL_GRAM(false, 4); else if (NCH == 2) GLL_GRAM(false, 2); else GLL_GRAM(false, 1);
+    }
+#undef GLL_GRAM
     prof_end(GLL_K_GRAM, s);
     return hipGetLastError();
 }
@@ -421,16 +480,25 @@ hipError_t launch_select(const Layout& L, void* ws, const float* X, float eps_fi
     if (kc > n - 1) kc = n - 1;
     dim3 grid((n + 3) / 4);
     prof_begin(GLL_K_SELECT, s);
-#define GLL_SEL(KCV, V)                                                                        \
-    knn_select_kernel<KCV, V><<<grid, 256, 0, s>>>(                                            \
-        L.at<float>(ws, L.D2), L.ldD, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0, L.RCAP,    \
+    const size_t plane = size_t(n) * L.ldD;
+#define GLL_SEL3(KCV, V, NPV)                                                                  \
+    knn_select_kernel<KCV, V, NPV><<<grid, 256, 0, s>>>(                                       \
+        L.at<float>(ws, L.D2), L.ldD, plane, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0,     \
+        L.RCAP,                                                                                \
         L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \
         L.at<int32_t>(ws, L.rev_cnt), L.at<int32_t>(ws, L.rev_idx), L.at<float>(ws, L.rev_d2), \
         L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub)
+#define GLL_SEL(KCV, V)                                                                        \
+    do {                                                                                       \
+        if (L.KS == 4) GLL_SEL3(KCV, V, 4);                                                    \
+        else if (L.KS == 2) GLL_SEL3(KCV, V, 2);                                               \
+        else GLL_SEL3(KCV, V, 1);                                                              \
+    } while (0)
     if (KC == 16) { if (vec) GLL_SEL(16, true); else GLL_SEL(16, false); }
     else if (KC == 32) { if (vec) GLL_SEL(32, true); else GLL_SEL(32, false); }
     else { if (vec) GLL_SEL(64, true); else GLL_SEL(64, false); }
 #undef GLL_SEL
+#undef GLL_SEL3
     prof_end(GLL_K_SELECT, s);
     return hipGetLastError();
 }

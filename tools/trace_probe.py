@@ -78,6 +78,19 @@ def timeline(tr, label):
         print(f"{kn:10s} {TICK_US * (a - t0):7.2f} -> {TICK_US * (b - t0):7.2f}  "
               f"({TICK_US * (b - a):6.2f}){gap}")
         prev = b
+    for u, (_, kns) in UNITS.items():
+        for i, kn in enumerate(kns):
+            last = int(tr[u][24 + i])
+            if last:
+                print(f"  {kn}: last workgroup entered at +{TICK_US * (last - int(tr[u][32 + 2 * i])):.2f}")
+    g = tr[0].astype(np.int64)
+    if g[10]:
+        print("gram block 0: " + ", ".join(f"{nm} +{TICK_US * (g[q] - g[10]):.2f}" for q, nm in
+                                          [(15, "chunk0 in LDS"), (11, "mfma done"), (12, "loop exit"),
+                                           (13, "tile staged"), (14, "stored")] if g[q]))
+    if g[16]:
+        print("select wave 0: " + ", ".join(f"{nm} +{TICK_US * (g[q] - g[16]):.2f}" for q, nm in
+                                           [(17, "merged"), (18, "refined"), (19, "ranked+written")] if g[q]))
     pts = tr[2][:10].astype(np.int64)
     if pts[0]:
         print("cg block 0: " + ", ".join(f"{CG_PTS[i]} +{TICK_US * (pts[i] - pts[0]):.2f}"
