@@ -16,7 +16,9 @@ Deliberate differences from the reference (all documented in DESIGN.md):
   * kNN is exact (the reference's annoy index is approximate);
   * the solves are fp32 Jacobi-CG to rtol 1e-6 instead of float64 SuperLU;
   * outputs are placed on X.device (the reference uses the *current* device, GLL.py:15-18);
-  * an optional 5th positional argument `k` replaces the hard-coded k=25 (GLL.py:27).
+  * an optional 5th positional argument `k` replaces the hard-coded k=25 (GLL.py:27);
+  * X may carry a leading batch dimension (B x n x d, labels B x base x C or shared):
+    B independent graphs in one launch per kernel, U is B x m x C.
 """
 from __future__ import annotations
 
@@ -200,24 +202,33 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
     def forward(ctx, X, label_matrix, tau=0, epsilon="auto", k=DEFAULT_K):
         _poll_status()
         dev = _device_for(X)
-        n, d = X.shape
-        base, C = label_matrix.shape
+        if X.dim() not in (2, 3) or label_matrix.dim() not in (2, X.dim()):
+            raise ValueError("X must be n x d (or B x n x d), label_matrix base x C "
+                             "(or B x base x C)")
+        B = X.shape[0] if X.dim() == 3 else 1
+        n, d = X.shape[-2:]
+        base, C = label_matrix.shape[-2:]
         with torch.cuda.device(dev):
             X32 = _features(X, dev)
             Y, ydt = _typed(label_matrix, dev)
+            if X.dim() == 3 and Y.dim() == 2:
+                Y = Y.unsqueeze(0).expand(B, base, C).contiguous()   # shared labels
+            if X.dim() == 3 and Y.shape[0] != B:
+                raise ValueError(f"label_matrix batch {Y.shape[0]} != {B}")
             prob = make_problem(n, d, base, C, k, tau, epsilon)
             prob.status_sink = _sink(dev)[0].data_ptr()
             nbytes = _lib.lib().gll_workspace_bytes(ct.byref(prob))
             if nbytes == 0:
                 raise ValueError(f"unsupported GLL problem n={n} d={d} base={base} C={C} k={k}")
-            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-            U = torch.empty(n - base, C, dtype=torch.float64, device=dev)
-            _lib.check(_lib.lib().gll_forward(ct.byref(prob), X32.data_ptr(), Y.data_ptr(), ydt,
-                                              ws.data_ptr(), U.data_ptr(), _stream(dev)),
+            ws = torch.empty(nbytes * B, dtype=torch.uint8, device=dev)
+            U = torch.empty(X.shape[:-2] + (n - base, C), dtype=torch.float64, device=dev)
+            _lib.check(_lib.lib().gll_forward_batched(ct.byref(prob), B, X32.data_ptr(),
+                                                      Y.data_ptr(), ydt, ws.data_ptr(),
+                                                      U.data_ptr(), _stream(dev)),
                        "gll_forward")
             _after_call(dev)
         ctx.save_for_backward(X)
-        ctx.prob, ctx.ws, ctx.dev = prob, ws, dev
+        ctx.prob, ctx.ws, ctx.dev, ctx.B = prob, ws, dev, B
         return U if X.is_cuda else U.cpu()
 
     @staticmethod
@@ -229,10 +240,10 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
             g, gdt = _typed(grad_output, dev)
             if gdt == _lib.GLL_DT_I64:
                 g, gdt = g.double(), _lib.GLL_DT_F64
-            gradX = torch.empty(prob.n, prob.d, dtype=torch.float32, device=dev)
-            _lib.check(_lib.lib().gll_backward(ct.byref(prob), X32.data_ptr(), None, 0,
-                                               ctx.ws.data_ptr(), g.data_ptr(), gdt,
-                                               gradX.data_ptr(), _stream(dev)),
+            gradX = torch.empty(X.shape, dtype=torch.float32, device=dev)
+            _lib.check(_lib.lib().gll_backward_batched(ct.byref(prob), ctx.B, X32.data_ptr(),
+                                                       ctx.ws.data_ptr(), g.data_ptr(), gdt,
+                                                       gradX.data_ptr(), _stream(dev)),
                        "gll_backward")
         if gradX.device != X.device or gradX.dtype != X.dtype:
             gradX = gradX.to(device=X.device, dtype=X.dtype)

@@ -21,7 +21,8 @@ K_COUNT = 6
 
 # every symbol include/gll.h declares (tests check the library exports all of them)
 EXPORTS = (
-    "gll_workspace_bytes", "gll_forward", "gll_backward", "gll_graph", "gll_workspace_view",
+    "gll_workspace_bytes", "gll_forward", "gll_backward", "gll_forward_batched",
+    "gll_backward_batched", "gll_graph", "gll_workspace_view",
     "gll_cg_csr_workspace_bytes", "gll_cg_csr", "gll_prof_enable", "gll_prof_read",
     "gll_kernel_name", "gll_strerror",
 )
@@ -54,6 +55,10 @@ def _declare(lib):
     lib.gll_forward.restype = i32
     lib.gll_backward.argtypes = [P, vp, vp, i32, vp, vp, i32, vp, vp]
     lib.gll_backward.restype = i32
+    lib.gll_forward_batched.argtypes = [P, i32, vp, vp, i32, vp, vp, vp]
+    lib.gll_forward_batched.restype = i32
+    lib.gll_backward_batched.argtypes = [P, i32, vp, vp, vp, i32, vp, vp]
+    lib.gll_backward_batched.restype = i32
     lib.gll_graph.argtypes = [P, vp, vp, vp]
     lib.gll_graph.restype = i32
     lib.gll_workspace_view.argtypes = [P, vp, ct.POINTER(View)]

@@ -90,15 +90,77 @@ static int32_t* public_status(const gll_problem* p, const Layout& L, void* ws) {
     return p->status_sink ? p->status_sink : L.at<int32_t>(ws, L.status);
 }
 
+static size_t dtype_size(int dt) { return dt == GLL_DT_F32 ? 4 : 8; }
+
+// Strides of B contiguous problems: workspace blocks of L.total bytes, X / Y / U / gbar /
+// gradX packed graph after graph; status words shared when they go to a sink.
+static Batch make_batch(const gll_problem* p, const Layout& L, int B, int y_dtype, int g_dtype) {
+    Batch bt;
+    bt.B = B;
+    bt.ws = L.total;
+    bt.x = size_t(L.n) * L.d * sizeof(float);
+    bt.y = size_t(L.base) * L.C * dtype_size(y_dtype);
+    bt.u = size_t(L.m) * L.C * sizeof(double);
+    bt.g = size_t(L.m) * L.C * dtype_size(g_dtype);
+    bt.gx = bt.x;
+    bt.st = p->status_sink ? 0 : L.total;
+    return bt;
+}
+
 // kNN graph: gram (MFMA) -> select (+ reverse scatter) -> row build (+ weights, rhs)
-static int build_graph(const gll_problem* p, const Layout& L, const float* X, const void* Y,
-                       int y_dtype, void* ws, hipStream_t s) {
+static int build_graph(const gll_problem* p, const Layout& L, const Batch& bt, const float* X,
+                       const void* Y, int y_dtype, void* ws, hipStream_t s) {
     const bool vec = vec_ok(X, p->d);
     const bool auto_eps = !(p->eps > 0.f);
-    if (launch_gram(L, ws, X, vec, s) != hipSuccess) return GLL_ERR_HIP;
-    if (launch_select(L, ws, X, p->eps, auto_eps, vec, public_status(p, L, ws), s) != hipSuccess)
+    if (launch_gram(L, bt, ws, X, vec, s) != hipSuccess) return GLL_ERR_HIP;
+    if (launch_select(L, bt, ws, X, p->eps, auto_eps, vec, public_status(p, L, ws), s) !=
+        hipSuccess)
         return GLL_ERR_HIP;
-    return hip_status(launch_finalize(L, ws, Y, y_dtype, p->tau, s));
+    return hip_status(launch_finalize(L, bt, ws, Y, y_dtype, p->tau, s));
+}
+
+static int forward_impl(const gll_problem* p, int B, const float* X, const void* Y, int y_dtype,
+                        void* ws, double* U, void* stream) {
+    int rc = check(p);
+    if (rc != GLL_OK) return rc;
+    if (B < 1 || B > 65535) return GLL_ERR_INVALID_ARG;
+    if (!X || !ws || (p->base > 0 && !Y) || (p->n > p->base && !U)) return GLL_ERR_INVALID_ARG;
+    if (y_dtype != GLL_DT_F32 && y_dtype != GLL_DT_F64 && y_dtype != GLL_DT_I64)
+        return GLL_ERR_INVALID_ARG;
+    Layout L(*p);
+    const Batch bt = make_batch(p, L, B, y_dtype, GLL_DT_F32);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    rc = build_graph(p, L, bt, X, Y, y_dtype, ws, s);
+    if (rc != GLL_OK) return rc;
+    const float rtol = p->rtol > 0.f ? p->rtol : 1e-6f;
+    const int max_iter = p->max_iter > 0 ? p->max_iter : 1000;
+    int32_t* st = public_status(p, L, ws);
+    float* U32 = L.at<float>(ws, L.P) + size_t(L.base) * L.C;
+    return hip_status(launch_cg_luu(L, bt, ws, L.at<float>(ws, L.rhs), bt.ws, GLL_DT_F32, U, U32,
+                                    rtol, max_iter, st + GLL_ST_FWD_NONCONV,
+                                    st + GLL_ST_FWD_ITERS, s));
+}
+
+static int backward_impl(const gll_problem* p, int B, const float* X, void* ws,
+                         const void* gbar, int g_dtype, float* gradX, void* stream) {
+    int rc = check(p);
+    if (rc != GLL_OK) return rc;
+    if (B < 1 || B > 65535) return GLL_ERR_INVALID_ARG;
+    if (!X || !ws || !gradX || (p->n > p->base && !gbar)) return GLL_ERR_INVALID_ARG;
+    if (g_dtype != GLL_DT_F32 && g_dtype != GLL_DT_F64) return GLL_ERR_INVALID_ARG;
+    Layout L(*p);
+    const Batch bt = make_batch(p, L, B, GLL_DT_F32, g_dtype);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const float rtol = p->rtol > 0.f ? p->rtol : 1e-6f;
+    const int max_iter = p->max_iter > 0 ? p->max_iter : 1000;
+    int32_t* st = public_status(p, L, ws);
+    float* wU = L.at<float>(ws, L.Wadj) + size_t(L.base) * L.C;
+    // adjoint solve: Luu is symmetric, so Luu^-T gbar = Luu^-1 gbar (GLL.py:93)
+    hipError_t e = launch_cg_luu(L, bt, ws, gbar, bt.g, g_dtype, nullptr, wU, rtol, max_iter,
+                                 st + GLL_ST_BWD_NONCONV, st + GLL_ST_BWD_ITERS, s);
+    if (e != hipSuccess) return GLL_ERR_HIP;
+    const bool auto_eps = !(p->eps > 0.f);
+    return hip_status(launch_backward_grad(L, bt, ws, X, auto_eps, gradX, vec_ok(X, p->d), s));
 }
 
 }  // namespace gll
@@ -119,46 +181,30 @@ int gll_graph(const gll_problem* p, const float* X, void* ws, void* stream) {
     if (p->base != 0) return GLL_ERR_INVALID_ARG;  // graph only: no labeled block
     Layout L(*p);
     // base = 0: every row is "unlabeled", rhs = 0 and no label is read
-    return build_graph(p, L, X, nullptr, GLL_DT_F32, ws, static_cast<hipStream_t>(stream));
+    return build_graph(p, L, make_batch(p, L, 1, GLL_DT_F32, GLL_DT_F32), X, nullptr, GLL_DT_F32,
+                       ws, static_cast<hipStream_t>(stream));
 }
 
 int gll_forward(const gll_problem* p, const float* X, const void* Y, int y_dtype, void* ws,
                 double* U, void* stream) {
-    int rc = check(p);
-    if (rc != GLL_OK) return rc;
-    if (!X || !ws || (p->base > 0 && !Y) || (p->n > p->base && !U)) return GLL_ERR_INVALID_ARG;
-    Layout L(*p);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    rc = build_graph(p, L, X, Y, y_dtype, ws, s);
-    if (rc != GLL_OK) return rc;
-    const float rtol = p->rtol > 0.f ? p->rtol : 1e-6f;
-    const int max_iter = p->max_iter > 0 ? p->max_iter : 1000;
-    int32_t* st = public_status(p, L, ws);
-    float* U32 = L.at<float>(ws, L.P) + size_t(L.base) * L.C;
-    return hip_status(launch_cg_luu(L, ws, L.at<float>(ws, L.rhs), GLL_DT_F32, U, U32, rtol,
-                                    max_iter, st + GLL_ST_FWD_NONCONV, st + GLL_ST_FWD_ITERS, s));
+    return forward_impl(p, 1, X, Y, y_dtype, ws, U, stream);
 }
 
 int gll_backward(const gll_problem* p, const float* X, const void* Y, int y_dtype, void* ws,
                  const void* gbar, int g_dtype, float* gradX, void* stream) {
     (void)Y;
     (void)y_dtype;
-    int rc = check(p);
-    if (rc != GLL_OK) return rc;
-    if (!X || !ws || !gradX || (p->n > p->base && !gbar)) return GLL_ERR_INVALID_ARG;
-    if (g_dtype != GLL_DT_F32 && g_dtype != GLL_DT_F64) return GLL_ERR_INVALID_ARG;
-    Layout L(*p);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    const float rtol = p->rtol > 0.f ? p->rtol : 1e-6f;
-    const int max_iter = p->max_iter > 0 ? p->max_iter : 1000;
-    int32_t* st = public_status(p, L, ws);
-    float* wU = L.at<float>(ws, L.Wadj) + size_t(L.base) * L.C;
-    // adjoint solve: Luu is symmetric, so Luu^-T gbar = Luu^-1 gbar (GLL.py:93)
-    hipError_t e = launch_cg_luu(L, ws, gbar, g_dtype, nullptr, wU, rtol, max_iter,
-                                 st + GLL_ST_BWD_NONCONV, st + GLL_ST_BWD_ITERS, s);
-    if (e != hipSuccess) return GLL_ERR_HIP;
-    const bool auto_eps = !(p->eps > 0.f);
-    return hip_status(launch_backward_grad(L, ws, X, auto_eps, gradX, vec_ok(X, p->d), s));
+    return backward_impl(p, 1, X, ws, gbar, g_dtype, gradX, stream);
+}
+
+int gll_forward_batched(const gll_problem* p, int B, const float* X, const void* Y, int y_dtype,
+                        void* ws, double* U, void* stream) {
+    return forward_impl(p, B, X, Y, y_dtype, ws, U, stream);
+}
+
+int gll_backward_batched(const gll_problem* p, int B, const float* X, void* ws, const void* gbar,
+                         int g_dtype, float* gradX, void* stream) {
+    return backward_impl(p, B, X, ws, gbar, g_dtype, gradX, stream);
 }
 
 int gll_workspace_view(const gll_problem* p, void* ws, gll_view* out) {

@@ -6,6 +6,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "gll.h"
 
 namespace gll {
@@ -304,23 +306,49 @@ __device__ __forceinline__ f32x4 mask4(f32x4 v, int k, int lim) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Batched launches: B independent graphs of the same shape in one launch per kernel, graph
+// g = blockIdx.y.  Every pointer a kernel receives is graph 0's; gshift moves it to graph g
+// by a per-array byte stride (0 = shared by all graphs, e.g. a status sink).
+// ---------------------------------------------------------------------------------------
+struct Batch {
+    int B = 1;
+    size_t ws = 0;   // workspace block
+    size_t x = 0;    // X (n x d fp32)
+    size_t y = 0;    // label matrix (base x C, its dtype)
+    size_t u = 0;    // U output (m x C fp64)
+    size_t g = 0;    // upstream gradient (m x C, its dtype)
+    size_t gx = 0;   // gradX output (n x d fp32)
+    size_t st = 0;   // public status words: ws when they live in the workspace, 0 for a sink
+};
+
+template <typename T>
+__device__ __forceinline__ T* gshift(T* p, size_t stride) {
+    if (p == nullptr || stride == 0) return p;
+    using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+    return reinterpret_cast<T*>(reinterpret_cast<B*>(p) + size_t(blockIdx.y) * stride);
+}
+
+// ---------------------------------------------------------------------------------------
 // Launchers (host side, one per translation unit)
 // ---------------------------------------------------------------------------------------
 void prof_begin(int kid, hipStream_t s);
 void prof_end(int kid, hipStream_t s);
 
-hipError_t launch_gram(const Layout& L, void* ws, const float* X, bool vec, hipStream_t s);
-hipError_t launch_select(const Layout& L, void* ws, const float* X, float eps_fixed,
-                         bool auto_eps, bool vec, int32_t* status_pub, hipStream_t s);
-hipError_t launch_finalize(const Layout& L, void* ws, const void* Y, int y_dtype, float tau,
-                           hipStream_t s);
-hipError_t launch_cg_luu(const Layout& L, void* ws, const void* b, int b_dtype, double* out64,
-                         float* out32, float rtol, int max_iter, int32_t* st_nonconv,
-                         int32_t* st_iters, hipStream_t s);
+hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
+                       hipStream_t s);
+hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float* X,
+                         float eps_fixed, bool auto_eps, bool vec, int32_t* status_pub,
+                         hipStream_t s);
+hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,
+                           int y_dtype, float tau, hipStream_t s);
+// b: right-hand sides of graph 0, `b_stride` bytes apart (the workspace rhs or gbar)
+hipError_t launch_cg_luu(const Layout& L, const Batch& bt, void* ws, const void* b,
+                         size_t b_stride, int b_dtype, double* out64, float* out32, float rtol,
+                         int max_iter, int32_t* st_nonconv, int32_t* st_iters, hipStream_t s);
 hipError_t launch_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col,
                          const float* val, const float* b, float* x, float atol, int max_iter,
                          int32_t* iters, int32_t* nonconv, float* gvec, hipStream_t s);
-hipError_t launch_backward_grad(const Layout& L, void* ws, const float* X, bool auto_eps,
-                                float* gradX, bool vec, hipStream_t s);
+hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, const float* X,
+                                bool auto_eps, float* gradX, bool vec, hipStream_t s);
 
 }  // namespace gll

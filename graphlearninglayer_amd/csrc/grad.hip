@@ -31,6 +31,21 @@ struct EdgeArgs {
     const int32_t* knn_idx;
     float* S;             // per-edge S (auto)
     float* b;             // per-row b (auto)
+    size_t wss;           // batched launches: workspace stride between graphs (bytes)
+
+    __device__ void to_graph() {   // move every workspace pointer to graph blockIdx.y
+        row_start = gshift(row_start, wss);
+        row_len = gshift(row_len, wss);
+        col = gshift(col, wss);
+        w = gshift(w, wss);
+        d2 = gshift(d2, wss);
+        eps = gshift(eps, wss);
+        P = gshift(P, wss);
+        Wadj = gshift(Wadj, wss);
+        knn_idx = gshift(knn_idx, wss);
+        S = gshift(S, wss);
+        b = gshift(b, wss);
+    }
 };
 
 // G_ij * V_ij for edge e = (i, j)
@@ -50,6 +65,7 @@ __device__ __forceinline__ float edge_gv(const EdgeArgs& a, int i, int j, float 
 // auto eps, pass 1: S_ij and b_i
 __global__ __launch_bounds__(256) void edge_coef_kernel(EdgeArgs a) {
     GLL_TRACE_SCOPE(0);
+    a.to_graph();
     const int lane = lane_id();
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
@@ -69,8 +85,12 @@ __global__ __launch_bounds__(256) void edge_coef_kernel(EdgeArgs a) {
 // out_i = (sum_e coef_e) x_i - sum_e coef_e x_{col_e};  AUTO selects the coefficient form
 template <bool AUTO, int ND, bool VEC>
 __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float* __restrict__ X,
-                                                        float* __restrict__ out) {
+                                                        float* __restrict__ out, size_t xs,
+                                                        size_t gxs) {
     GLL_TRACE_SCOPE(1);
+    a.to_graph();
+    X = gshift(X, xs);
+    out = gshift(out, gxs);
     const int lane = lane_id();
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
@@ -145,20 +165,23 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
 }
 
 template <bool AUTO, bool VEC>
-static hipError_t grad_nd(const EdgeArgs& a, const float* X, float* out, hipStream_t s) {
-    dim3 grid((a.n + 3) / 4);
+static hipError_t grad_nd(const EdgeArgs& a, const Batch& bt, const float* X, float* out,
+                          hipStream_t s) {
+    dim3 grid((a.n + 3) / 4, bt.B);
     const int nd = (a.d + 255) / 256;
-    if (nd <= 1) grad_spmm_kernel<AUTO, 1, VEC><<<grid, 256, 0, s>>>(a, X, out);
-    else if (nd <= 2) grad_spmm_kernel<AUTO, 2, VEC><<<grid, 256, 0, s>>>(a, X, out);
-    else if (nd <= 4) grad_spmm_kernel<AUTO, 4, VEC><<<grid, 256, 0, s>>>(a, X, out);
-    else if (nd <= 8) grad_spmm_kernel<AUTO, 8, VEC><<<grid, 256, 0, s>>>(a, X, out);
-    else if (nd <= 16) grad_spmm_kernel<AUTO, 16, VEC><<<grid, 256, 0, s>>>(a, X, out);
+#define GLL_GRAD(ND) grad_spmm_kernel<AUTO, ND, VEC><<<grid, 256, 0, s>>>(a, X, out, bt.x, bt.gx)
+    if (nd <= 1) GLL_GRAD(1);
+    else if (nd <= 2) GLL_GRAD(2);
+    else if (nd <= 4) GLL_GRAD(4);
+    else if (nd <= 8) GLL_GRAD(8);
+    else if (nd <= 16) GLL_GRAD(16);
     else return hipErrorInvalidValue;
+#undef GLL_GRAD
     return hipGetLastError();
 }
 
-hipError_t launch_backward_grad(const Layout& L, void* ws, const float* X, bool auto_eps,
-                                float* gradX, bool vec, hipStream_t s) {
+hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, const float* X,
+                                bool auto_eps, float* gradX, bool vec, hipStream_t s) {
     EdgeArgs a;
     a.n = L.n;
     a.base = L.base;
@@ -176,18 +199,20 @@ hipError_t launch_backward_grad(const Layout& L, void* ws, const float* X, bool 
     a.knn_idx = L.at<int32_t>(ws, L.knn_idx);
     a.S = L.at<float>(ws, L.S);
     a.b = L.at<float>(ws, L.b);
+    a.wss = bt.ws;
     hipError_t e;
     if (auto_eps) {
         prof_begin(GLL_K_EDGE, s);
-        edge_coef_kernel<<<(L.n + 3) / 4, 256, 0, s>>>(a);
+        edge_coef_kernel<<<dim3((L.n + 3) / 4, bt.B), 256, 0, s>>>(a);
         prof_end(GLL_K_EDGE, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         prof_begin(GLL_K_GRAD, s);
-        e = vec ? grad_nd<true, true>(a, X, gradX, s) : grad_nd<true, false>(a, X, gradX, s);
+        e = vec ? grad_nd<true, true>(a, bt, X, gradX, s) : grad_nd<true, false>(a, bt, X, gradX, s);
         prof_end(GLL_K_GRAD, s);
     } else {
         prof_begin(GLL_K_GRAD, s);
-        e = vec ? grad_nd<false, true>(a, X, gradX, s) : grad_nd<false, false>(a, X, gradX, s);
+        e = vec ? grad_nd<false, true>(a, bt, X, gradX, s)
+                : grad_nd<false, false>(a, bt, X, gradX, s);
         prof_end(GLL_K_GRAD, s);
     }
     return e;

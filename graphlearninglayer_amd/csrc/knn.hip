@@ -63,8 +63,13 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
                                                        float* __restrict__ D2, int ld,
                                                        size_t plane,
                                                        int32_t* __restrict__ status,
-                                                       int32_t* __restrict__ rev_cnt) {
+                                                       int32_t* __restrict__ rev_cnt,
+                                                       size_t xs, size_t wss) {
     GLL_TRACE_SCOPE(0);
+    X = gshift(X, xs);
+    D2 = gshift(D2, wss);
+    status = gshift(status, wss);
+    rev_cnt = gshift(rev_cnt, wss);
     // stage[buf][A|B][64 rows][kGL]; the epilogue reuses the same storage
     __shared__ __attribute__((aligned(16))) float smem[2 * 2 * 64 * kGL];
     __shared__ float s_sq[2][64];
@@ -330,8 +335,20 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     int kc, float eps_fixed, int auto_eps, int RCAP, int32_t* __restrict__ knn_idx,
     float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ rev_cnt,
     int32_t* __restrict__ rev_idx, float* __restrict__ rev_d2, int32_t* __restrict__ ovf,
-    int32_t* __restrict__ status, int32_t* __restrict__ status_pub) {
+    int32_t* __restrict__ status, int32_t* __restrict__ status_pub, size_t xs, size_t wss,
+    size_t sts) {
     GLL_TRACE_SCOPE(1);
+    D2 = gshift(D2, wss);
+    X = gshift(X, xs);
+    knn_idx = gshift(knn_idx, wss);
+    knn_d2 = gshift(knn_d2, wss);
+    eps = gshift(eps, wss);
+    rev_cnt = gshift(rev_cnt, wss);
+    rev_idx = gshift(rev_idx, wss);
+    rev_d2 = gshift(rev_d2, wss);
+    ovf = gshift(ovf, wss);
+    status = gshift(status, wss);
+    status_pub = gshift(status_pub, sts);
     const int lane = lane_id();
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;  // whole wave
@@ -441,7 +458,8 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     }
 }
 
-hipError_t launch_gram(const Layout& L, void* ws, const float* X, bool vec, hipStream_t s) {
+hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
+                       hipStream_t s) {
     const int T = (L.n + 63) / 64;
     const int tiles = T * (T + 1) / 2;
     const int KS = L.KS;
@@ -453,10 +471,11 @@ hipError_t launch_gram(const Layout& L, void* ws, const float* X, bool vec, hipS
     const size_t plane = size_t(L.n) * L.ldD;
     int32_t* st = L.at<int32_t>(ws, L.status);
     int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
-    const dim3 grid(tiles * KS);
+    const dim3 grid(tiles * KS, bt.B);
     prof_begin(GLL_K_GRAM, s);
 #define GLL_GRAM(V, N) \
-    gram_lds_kernel<V, N><<<grid, 512, 0, s>>>(X, L.n, L.d, T, KS, kspan, D2, L.ldD, plane, st, rc)
+    gram_lds_kernel<V, N><<<grid, 512, 0, s>>>(X, L.n, L.d, T, KS, kspan, D2, L.ldD, plane, st, \
+                                                rc, bt.x, bt.ws)
     if (vec) {
         if (NCH == 4) GLL_GRAM(true, 4); else if (NCH == 2) GLL_GRAM(true, 2); else GLL_GRAM(true, 1);
     } else {
@@ -467,8 +486,9 @@ hipError_t launch_gram(const Layout& L, void* ws, const float* X, bool vec, hipS
     return hipGetLastError();
 }
 
-hipError_t launch_select(const Layout& L, void* ws, const float* X, float eps_fixed,
-                         bool auto_eps, bool vec, int32_t* status_pub, hipStream_t s) {
+hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float* X,
+                         float eps_fixed, bool auto_eps, bool vec, int32_t* status_pub,
+                         hipStream_t s) {
     const int n = L.n, K = L.K;
     // candidate list capacity: smallest of {16, 32, 64} leaving a re-rank margin >= 4
     const int need = K - 1 + 4;
@@ -478,7 +498,7 @@ hipError_t launch_select(const Layout& L, void* ws, const float* X, float eps_fi
     if (margin > 8) margin = 8;
     int kc = K - 1 + margin;
     if (kc > n - 1) kc = n - 1;
-    dim3 grid((n + 3) / 4);
+    dim3 grid((n + 3) / 4, bt.B);
     prof_begin(GLL_K_SELECT, s);
     const size_t plane = size_t(n) * L.ldD;
 #define GLL_SEL3(KCV, V, NPV)                                                                  \
@@ -487,7 +507,7 @@ hipError_t launch_select(const Layout& L, void* ws, const float* X, float eps_fi
         L.RCAP,                                                                                \
         L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \
         L.at<int32_t>(ws, L.rev_cnt), L.at<int32_t>(ws, L.rev_idx), L.at<float>(ws, L.rev_d2), \
-        L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub)
+        L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub, bt.x, bt.ws, bt.st)
 #define GLL_SEL(KCV, V)                                                                        \
     do {                                                                                       \
         if (L.KS == 4) GLL_SEL3(KCV, V, 4);                                                    \

@@ -47,6 +47,31 @@ struct RowArgs {
     float* rhs;
     float* P;
     float* Wadj;
+    size_t wss;   // batched launches: workspace stride between graphs (bytes)
+
+    __device__ void to_graph() {   // move every workspace pointer to graph blockIdx.y
+        knn_idx = gshift(knn_idx, wss);
+        knn_d2 = gshift(knn_d2, wss);
+        rev_cnt = gshift(rev_cnt, wss);
+        rev_idx = gshift(rev_idx, wss);
+        rev_d2 = gshift(rev_d2, wss);
+        ovf = gshift(ovf, wss);
+        status = gshift(status, wss);
+        eps = gshift(eps, wss);
+        tmp_col = gshift(tmp_col, wss);
+        tmp_d2 = gshift(tmp_d2, wss);
+        row_start = gshift(row_start, wss);
+        row_len = gshift(row_len, wss);
+        col = gshift(col, wss);
+        w = gshift(w, wss);
+        d2e = gshift(d2e, wss);
+        deg = gshift(deg, wss);
+        ucnt = gshift(ucnt, wss);
+        diag = gshift(diag, wss);
+        rhs = gshift(rhs, wss);
+        P = gshift(P, wss);
+        Wadj = gshift(Wadj, wss);
+    }
 };
 
 template <typename TY>
@@ -184,8 +209,11 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
 }
 
 template <typename TY>
-__global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __restrict__ Y) {
+__global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __restrict__ Y,
+                                                        size_t ys) {
     GLL_TRACE_SCOPE(0);
+    a.to_graph();
+    Y = gshift(Y, ys);
     __shared__ int s_col[4][kStage];
     __shared__ float s_d2[4][kStage];
     __shared__ int t_col[4][kStage];
@@ -221,8 +249,8 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
                              nullptr, nullptr, nullptr);
 }
 
-hipError_t launch_finalize(const Layout& L, void* ws, const void* Y, int y_dtype, float tau,
-                           hipStream_t s) {
+hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,
+                           int y_dtype, float tau, hipStream_t s) {
     if (L.C > kMaxCPerLane * kWave) return hipErrorInvalidValue;
     RowArgs a;
     a.n = L.n;
@@ -254,11 +282,12 @@ hipError_t launch_finalize(const Layout& L, void* ws, const void* Y, int y_dtype
     a.rhs = L.at<float>(ws, L.rhs);
     a.P = L.at<float>(ws, L.P);
     a.Wadj = L.at<float>(ws, L.Wadj);
-    dim3 grid((L.n + 3) / 4);
+    a.wss = bt.ws;
+    dim3 grid((L.n + 3) / 4, bt.B);
     prof_begin(GLL_K_FINALIZE, s);
-    if (y_dtype == GLL_DT_F32) row_build_kernel<float><<<grid, 256, 0, s>>>(a, static_cast<const float*>(Y));
-    else if (y_dtype == GLL_DT_F64) row_build_kernel<double><<<grid, 256, 0, s>>>(a, static_cast<const double*>(Y));
-    else if (y_dtype == GLL_DT_I64) row_build_kernel<int64_t><<<grid, 256, 0, s>>>(a, static_cast<const int64_t*>(Y));
+    if (y_dtype == GLL_DT_F32) row_build_kernel<float><<<grid, 256, 0, s>>>(a, static_cast<const float*>(Y), bt.y);
+    else if (y_dtype == GLL_DT_F64) row_build_kernel<double><<<grid, 256, 0, s>>>(a, static_cast<const double*>(Y), bt.y);
+    else if (y_dtype == GLL_DT_I64) row_build_kernel<int64_t><<<grid, 256, 0, s>>>(a, static_cast<const int64_t*>(Y), bt.y);
     else return hipErrorInvalidValue;
     prof_end(GLL_K_FINALIZE, s);
     return hipGetLastError();

@@ -101,8 +101,19 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     const int32_t* __restrict__ col, const float* __restrict__ wv, const float* __restrict__ diag,
     const TB* __restrict__ bsrc, double* __restrict__ out64, float* __restrict__ out32,
     float rtol, int max_iter, int mat_cap, int32_t* __restrict__ st_nonconv,
-    int32_t* __restrict__ st_iters) {
+    int32_t* __restrict__ st_iters, size_t wss, size_t bs, size_t us, size_t sts) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
+    row_start = gshift(row_start, wss);   // batched launches: graph blockIdx.y
+    row_len = gshift(row_len, wss);
+    ucnt = gshift(ucnt, wss);
+    col = gshift(col, wss);
+    wv = gshift(wv, wss);
+    diag = gshift(diag, wss);
+    bsrc = gshift(bsrc, bs);
+    out64 = gshift(out64, us);
+    out32 = gshift(out32, wss);
+    st_nonconv = gshift(st_nonconv, sts);
+    st_iters = gshift(st_iters, sts);
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
     float* red = smem;                                  // 4 x 16 floats of reduction scratch
@@ -255,8 +266,20 @@ __global__ __launch_bounds__(NT) void cg_lds_kernel(
     const float* __restrict__ wv, const float* __restrict__ diag, const TB* __restrict__ bsrc,
     double* __restrict__ out64, float* __restrict__ out32, float rtol, int max_iter,
     float* __restrict__ gvec, int vec_in_lds, int32_t* __restrict__ st_nonconv,
-    int32_t* __restrict__ st_iters) {
+    int32_t* __restrict__ st_iters, size_t wss, size_t bs, size_t us, size_t sts) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
+    row_start = gshift(row_start, wss);
+    row_len = gshift(row_len, wss);
+    ucnt = gshift(ucnt, wss);
+    col = gshift(col, wss);
+    wv = gshift(wv, wss);
+    diag = gshift(diag, wss);
+    bsrc = gshift(bsrc, bs);
+    out64 = gshift(out64, us);
+    out32 = gshift(out32, wss);
+    gvec = gshift(gvec, wss);
+    st_nonconv = gshift(st_nonconv, sts);
+    st_iters = gshift(st_iters, sts);
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
     float* red = smem;
@@ -326,9 +349,9 @@ __global__ __launch_bounds__(NT) void cg_lds_kernel(
 
 
 template <int NT, int R, int S, typename TB>
-static hipError_t run_ell(const Layout& L, void* ws, const TB* b, double* out64, float* out32,
-                          float rtol, int max_iter, int32_t* st_nonconv, int32_t* st_iters,
-                          hipStream_t s) {
+static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* b, size_t bs,
+                          double* out64, float* out32, float rtol, int max_iter,
+                          int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
     size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4;
     // entries past the ELL slices: at most (m + n)(K-1) U-block entries in all
     const int64_t eu_bound = int64_t(L.m + L.n) * (L.K - 1);
@@ -338,21 +361,22 @@ static hipError_t run_ell(const Layout& L, void* ws, const TB* b, double* out64,
     lds += size_t(cap) * 8;
     auto fn = cg_ell_kernel<NT, R, S, TB>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
-    fn<<<L.C, NT, lds, s>>>(L.m, L.C, L.base, L.at<int32_t>(ws, L.row_start),
-                            L.at<int32_t>(ws, L.row_len), L.at<int32_t>(ws, L.ucnt),
-                            L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
-                            L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, int(cap),
-                            st_nonconv, st_iters);
+    fn<<<dim3(L.C, bt.B), NT, lds, s>>>(
+        L.m, L.C, L.base, L.at<int32_t>(ws, L.row_start), L.at<int32_t>(ws, L.row_len),
+        L.at<int32_t>(ws, L.ucnt), L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
+        L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, int(cap), st_nonconv, st_iters,
+        bt.ws, bs, bt.u, bt.st);
     return hipGetLastError();
 }
 
 template <typename TB>
-static hipError_t cg_dispatch(const Layout& L, void* ws, const TB* b, double* out64,
-                              float* out32, float rtol, int max_iter, int32_t* st_nonconv,
-                              int32_t* st_iters, hipStream_t s) {
+static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const TB* b, size_t bs,
+                              double* out64, float* out32, float rtol, int max_iter,
+                              int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
     const int m = L.m;
-#define GLL_ELL(NT, R, S) \
-    return run_ell<NT, R, S, TB>(L, ws, b, out64, out32, rtol, max_iter, st_nonconv, st_iters, s)
+#define GLL_ELL(NT, R, S)                                                                   \
+    return run_ell<NT, R, S, TB>(L, bt, ws, b, bs, out64, out32, rtol, max_iter, st_nonconv, \
+                                 st_iters, s)
     if (m <= 64) GLL_ELL(64, 1, 24);
     if (m <= 128) GLL_ELL(128, 1, 24);
     if (m <= 256) GLL_ELL(256, 1, 24);
@@ -366,26 +390,26 @@ static hipError_t cg_dispatch(const Layout& L, void* ws, const TB* b, double* ou
     const size_t lds = 64 * 4 + (vec_lds ? vec_bytes : 0);
     auto fn = cg_lds_kernel<1024, TB>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
-    fn<<<L.C, 1024, lds, s>>>(m, L.C, L.base, L.at<int32_t>(ws, L.row_start),
-                              L.at<int32_t>(ws, L.row_len), L.at<int32_t>(ws, L.ucnt),
-                              L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
-                              L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter,
-                              L.at<float>(ws, L.cgv), vec_lds ? 1 : 0, st_nonconv, st_iters);
+    fn<<<dim3(L.C, bt.B), 1024, lds, s>>>(
+        m, L.C, L.base, L.at<int32_t>(ws, L.row_start), L.at<int32_t>(ws, L.row_len),
+        L.at<int32_t>(ws, L.ucnt), L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
+        L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, L.at<float>(ws, L.cgv),
+        vec_lds ? 1 : 0, st_nonconv, st_iters, bt.ws, bs, bt.u, bt.st);
     return hipGetLastError();
 }
 
-hipError_t launch_cg_luu(const Layout& L, void* ws, const void* b, int b_dtype, double* out64,
-                         float* out32, float rtol, int max_iter, int32_t* st_nonconv,
-                         int32_t* st_iters, hipStream_t s) {
+hipError_t launch_cg_luu(const Layout& L, const Batch& bt, void* ws, const void* b,
+                         size_t b_stride, int b_dtype, double* out64, float* out32, float rtol,
+                         int max_iter, int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
     if (L.m <= 0) return hipSuccess;
     hipError_t e;
     prof_begin(GLL_K_CG, s);
     if (b_dtype == GLL_DT_F32)
-        e = cg_dispatch(L, ws, static_cast<const float*>(b), out64, out32, rtol, max_iter,
-                        st_nonconv, st_iters, s);
+        e = cg_dispatch(L, bt, ws, static_cast<const float*>(b), b_stride, out64, out32, rtol,
+                        max_iter, st_nonconv, st_iters, s);
     else if (b_dtype == GLL_DT_F64)
-        e = cg_dispatch(L, ws, static_cast<const double*>(b), out64, out32, rtol, max_iter,
-                        st_nonconv, st_iters, s);
+        e = cg_dispatch(L, bt, ws, static_cast<const double*>(b), b_stride, out64, out32, rtol,
+                        max_iter, st_nonconv, st_iters, s);
     else
         return hipErrorInvalidValue;
     prof_end(GLL_K_CG, s);

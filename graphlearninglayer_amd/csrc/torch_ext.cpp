@@ -6,6 +6,9 @@
 // GPU spends on the whole call, so the node lives here in C++: forward/backward marshal the
 // tensors (device, dtype, contiguity), take the workspace from the caching allocator and
 // call gll_forward / gll_backward on the current HIP stream.  No numerics here.
+// A leading batch dimension (X: B x n x d, label_matrix: B x base x C or shared base x C)
+// runs B independent graphs through gll_forward_batched / gll_backward_batched: one launch
+// per kernel for all B.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
@@ -57,24 +60,30 @@ class LaplaceLearningFn : public torch::autograd::Function<LaplaceLearningFn> {
     static at::Tensor forward(AutogradContext* ctx, const at::Tensor& X, const at::Tensor& Y,
                               double tau, double eps, int64_t k, int64_t max_iter, double rtol,
                               int64_t sink) {
-        TORCH_CHECK(X.dim() == 2 && Y.dim() == 2, "X and label_matrix must be 2-D");
+        TORCH_CHECK((X.dim() == 2 || X.dim() == 3) && (Y.dim() == 2 || Y.dim() == X.dim()),
+                    "X must be n x d (or B x n x d) and label_matrix base x C (or B x base x C)");
+        const bool batched = X.dim() == 3;
+        const int64_t B = batched ? X.size(0) : 1;
         const c10::Device dev =
             X.is_cuda() ? X.device() : c10::Device(c10::kCUDA, c10::hip::current_device());
         c10::DeviceGuard guard(dev);
         at::Tensor X32 = features(X, dev);
-        at::Tensor Yd = Y.detach().to(dev).contiguous();
+        at::Tensor Yd = Y.detach().to(dev);
         const int ycode = dtype_code(Yd);
+        const int64_t n = X.size(-2), d = X.size(-1), base = Y.size(-2), C = Y.size(-1);
+        if (batched && Y.dim() == 2) Yd = Yd.unsqueeze(0).expand({B, base, C});   // shared labels
+        TORCH_CHECK(!batched || Yd.size(0) == B, "label_matrix batch ", Yd.size(0), " != ", B);
         Yd = Yd.contiguous();
-        const int64_t n = X.size(0), d = X.size(1), base = Y.size(0), C = Y.size(1);
         gll_problem p = make_problem(n, d, base, C, k, tau, eps, max_iter, rtol, sink);
         const size_t nb = gll_workspace_bytes(&p);
         TORCH_CHECK(nb > 0, "unsupported GLL problem n=", n, " d=", d, " base=", base,
                     " C=", C, " k=", k);
-        at::Tensor ws = at::empty({int64_t(nb)}, X32.options().dtype(at::kByte));
-        at::Tensor U = at::empty({n - base, C}, X32.options().dtype(at::kDouble));
+        at::Tensor ws = at::empty({int64_t(nb) * B}, X32.options().dtype(at::kByte));
+        at::Tensor U = batched ? at::empty({B, n - base, C}, X32.options().dtype(at::kDouble))
+                               : at::empty({n - base, C}, X32.options().dtype(at::kDouble));
         hipStream_t s = c10::hip::getCurrentHIPStream(dev.index()).stream();
-        check_rc(gll_forward(&p, X32.data_ptr<float>(), Yd.data_ptr(), ycode, ws.data_ptr(),
-                             U.data_ptr<double>(), s),
+        check_rc(gll_forward_batched(&p, int(B), X32.data_ptr<float>(), Yd.data_ptr(), ycode,
+                                     ws.data_ptr(), U.data_ptr<double>(), s),
                  "gll_forward");
         ctx->save_for_backward({X});
         ctx->saved_data["ws"] = ws;
@@ -94,8 +103,9 @@ class LaplaceLearningFn : public torch::autograd::Function<LaplaceLearningFn> {
         at::Tensor ws = ctx->saved_data["ws"].toTensor();
         const c10::Device dev = ws.device();
         c10::DeviceGuard guard(dev);
+        const int64_t B = X.dim() == 3 ? X.size(0) : 1;
         gll_problem p = make_problem(
-            X.size(0), X.size(1), ctx->saved_data["base"].toInt(), ctx->saved_data["C"].toInt(),
+            X.size(-2), X.size(-1), ctx->saved_data["base"].toInt(), ctx->saved_data["C"].toInt(),
             ctx->saved_data["k"].toInt(), ctx->saved_data["tau"].toDouble(),
             ctx->saved_data["eps"].toDouble(), ctx->saved_data["max_iter"].toInt(),
             ctx->saved_data["rtol"].toDouble(), ctx->saved_data["sink"].toInt());
@@ -104,10 +114,10 @@ class LaplaceLearningFn : public torch::autograd::Function<LaplaceLearningFn> {
         if (g.scalar_type() != at::kFloat && g.scalar_type() != at::kDouble) g = g.to(at::kDouble);
         g = g.contiguous();
         const int gcode = g.scalar_type() == at::kFloat ? GLL_DT_F32 : GLL_DT_F64;
-        at::Tensor gradX = at::empty({X.size(0), X.size(1)}, X32.options());
+        at::Tensor gradX = at::empty(X.sizes(), X32.options());
         hipStream_t s = c10::hip::getCurrentHIPStream(dev.index()).stream();
-        check_rc(gll_backward(&p, X32.data_ptr<float>(), nullptr, 0, ws.data_ptr(), g.data_ptr(),
-                              gcode, gradX.data_ptr<float>(), s),
+        check_rc(gll_backward_batched(&p, int(B), X32.data_ptr<float>(), ws.data_ptr(),
+                                      g.data_ptr(), gcode, gradX.data_ptr<float>(), s),
                  "gll_backward");
         if (gradX.device() != X.device() || gradX.scalar_type() != X.scalar_type())
             gradX = gradX.to(X.device(), X.scalar_type());

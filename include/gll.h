@@ -74,6 +74,18 @@ int gll_forward(const gll_problem* p, const float* X, const void* Y, int y_dtype
 int gll_backward(const gll_problem* p, const float* X, const void* Y, int y_dtype,
                  void* workspace, const void* gbar, int g_dtype, float* gradX, void* stream);
 
+/* Batched variants (no reference counterpart -- B independent calls of
+ * GLL.py:14-177 on graphs of one shape, e.g. the 6 PGD calls of one minibatch in
+ * train_and_adversarial.py:711-749, or one minibatch per rank-local stream).  Graph g reads
+ * X + g*n*d, Y + g*base*C and writes U + g*m*C (gbar + g*m*C, gradX + g*n*d in the
+ * backward); `workspace` holds B consecutive blocks of gll_workspace_bytes(p) bytes.  Each
+ * kernel is launched once for all B graphs (grid.y = graph), so small graphs fill the GPU.
+ * Results are bitwise those of B single calls.  1 <= B <= 65535. */
+int gll_forward_batched(const gll_problem* p, int B, const float* X, const void* Y, int y_dtype,
+                        void* workspace, double* U, void* stream);
+int gll_backward_batched(const gll_problem* p, int B, const float* X, void* workspace,
+                         const void* gbar, int g_dtype, float* gradX, void* stream);
+
 /* Graph only (the device half of knn_sym_dist, GLL.py:180-244): kNN search, symmetric
  * CSR, eps, weights and degrees into the workspace; no solve.  Requires p->base == 0
  * (no labeled block; size the workspace for that problem).  Read the arrays with

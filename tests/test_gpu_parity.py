@@ -272,3 +272,54 @@ def test_output_does_not_alias_saved_state():
         U.mul_(0.5).add_(1.0)
     (again,) = torch.autograd.grad(U, X, g)
     assert torch.equal(ref, again)
+
+
+def _synth_batch(cfg, B, seed0=0):
+    from graphlearninglayer_amd.synth import CONFIGS, one_hot, synth
+    c = CONFIGS[cfg]
+    Xs, Ys = [], []
+    for g in range(B):
+        X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=seed0 + g)
+        Xs.append(X)
+        Ys.append(one_hot(lab[: c["base"]]))
+    return np.stack(Xs), np.stack(Ys), c
+
+
+@pytest.mark.parametrize("cfg,eps,ydt", [("plumbing", "auto", "i64"), ("ns", 1.0, "f32")])
+def test_batched_graphs_equal_single_calls_bitwise(cfg, eps, ydt):
+    """B graphs in one launch per kernel give exactly B single calls."""
+    from graphlearninglayer_amd.synth import seeded_gbar
+    GLL = _gll()
+    B = 5
+    Xs, Ys, c = _synth_batch(cfg, B, seed0=11)
+    if ydt == "i64":
+        Ys = Ys.astype(np.int64)
+    G = np.stack([seeded_gbar(c["batch"], 10, 100 + g) for g in range(B)])
+    Xb = torch.from_numpy(Xs).cuda().requires_grad_(True)
+    Ub = GLL.LaplaceLearningSparseHard.apply(Xb, torch.from_numpy(Ys).cuda(), 0.07, eps, c["k"])
+    assert Ub.shape == (B, c["batch"], 10) and Ub.dtype == torch.float64
+    Ub.backward(torch.from_numpy(G).cuda())
+    for g in range(B):
+        U1, gx1 = _run(Xs[g], Ys[g], 0.07, eps, c["k"], G[g])
+        np.testing.assert_array_equal(Ub[g].detach().cpu().numpy(), U1)
+        np.testing.assert_array_equal(Xb.grad[g].cpu().numpy(), gx1)
+
+
+def test_batched_shared_labels_python_and_cpp_paths_agree():
+    GLL = _gll()
+    B = 3
+    Xs, Ys, c = _synth_batch("plumbing", B, seed0=3)
+    Y = torch.from_numpy(Ys[0]).cuda()            # one label matrix shared by the batch
+    outs = []
+    for fn in (GLL.LaplaceLearningSparseHard.apply, GLL.LaplaceLearningSparseHard.apply_python):
+        Xb = torch.from_numpy(Xs).cuda().requires_grad_(True)
+        U = fn(Xb, Y, 0.0, 1.0, c["k"])
+        (gx,) = torch.autograd.grad(U.sum(), Xb)
+        outs.append((U.detach().cpu().numpy(), gx.cpu().numpy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    # every graph against the float64 oracle on the GPU's own kNN lists
+    for g in range(B):
+        ind = _gpu_knn(Xs[g], c["k"], 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+        Uo, _ = O.forward(Xs[g], Ys[0], tau=0.0, epsilon=1.0, K=c["k"], knn=(ind, None))
+        assert O.rel_err(outs[0][0][g], Uo) <= TOL
