@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the CPU-baseline sample (rank 0, N=1 only); 0 disables")
     ap.add_argument("--no-profile", action="store_true", help="skip kernel event timing")
+    ap.add_argument("--batch", type=int, default=64,
+                    help="graphs per launch of the batched entry point measured beside the "
+                         "headline (SURVEY.md §8f-2); 0 disables")
     return ap.parse_args()
 
 
@@ -89,6 +92,52 @@ def pmc_traffic(config, kernel):
         if sym in doc["kernels"]:
             return round(doc["kernels"][sym]["traffic_bytes"], 1)
     return None
+
+
+def batched_measure(c, eps, tau, k, B, units, dev, rank, steps=20, warmup=5):
+    """B independent graphs of the workload per call of the batched entry point (X: B x n x d):
+    whole-batch fwd+bwd throughput, and the CG kernel against the HBM roofline, where one
+    launch now carries B graphs' SpMVs ('reported at batched NS')."""
+    distinct = min(B, 8)   # a few distinct graphs, tiled: timing does not depend on content
+    Xs, Ys = [], []
+    for g in range(distinct):
+        X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=1000 * rank + g)
+        Xs.append(X)
+        Ys.append(one_hot(lab[: c["base"]]))
+    reps = (B + distinct - 1) // distinct
+    Xb = torch.from_numpy(np.concatenate([np.stack(Xs)] * reps)[:B]).to(dev).requires_grad_(True)
+    Yb = torch.from_numpy(np.concatenate([np.stack(Ys)] * reps)[:B]).to(dev)
+    G = torch.from_numpy(np.stack([seeded_gbar(c["batch"], 10, 1234 + g) for g in range(B)])).to(dev)
+    lap = GLL.LaplaceLearningSparseHard.apply
+
+    def step():
+        U = lap(Xb, Yb, tau, eps, k)
+        return torch.autograd.grad(U, Xb, G)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    kid = [_lib.kernel_name(q) for q in range(_lib.K_COUNT)].index("cg_kernel")
+    _lib.prof_enable(kid, 1)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms, cnt = _lib.prof_read(kid)
+    _lib.prof_enable(kid, 0)
+    bound, work = units["cg_kernel"]
+    avg_s = ms / cnt / 1e3
+    achieved = B * work / avg_s / 1e9
+    return {"B": B, "value": round(B * steps / elapsed, 3), "unit": "calls/s",
+            "ms_per_step": round(1e3 * elapsed / steps, 4),
+            "note": "one fwd+bwd of the batched entry point = B graphs; CG events cost ~2 us "
+                    "per launch, included",
+            "roofline": {"kernel": "cg_kernel", "bound": bound, "achieved": round(achieved, 3),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "work_per_launch": B * work, "avg_launch_us": round(avg_s * 1e6, 3),
+                         "launches": cnt}}
 
 
 def cpu_baseline(cfg, eps, tau, seconds):
@@ -217,6 +266,10 @@ def main():
             b_, w_ = units[kn]
             v["algorithmic"] = (f"{w_ / 1e9:.4g} GFLOP" if b_ == "mfma" else f"{w_ / 1e6:.4g} MB")
 
+    batched = None
+    if a.batch > 0 and roofline is not None:
+        batched = batched_measure(c, eps, tau, k, a.batch, units, dev, rank)
+
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         cpu = cpu_baseline(c, eps, tau, a.cpu_seconds)
@@ -243,6 +296,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels": per_kernel,
+            "batched": batched,
         }
         if roofline is not None:
             out["call_roofline"] = {"t_roof_us": round(call_roof_s * 1e6, 3),

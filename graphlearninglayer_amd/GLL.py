@@ -141,10 +141,10 @@ def _eps_value(epsilon) -> float:
 
 
 def make_problem(n, d, base, C, k=DEFAULT_K, tau=0.0, epsilon="auto",
-                 rtol=DEFAULT_RTOL, max_iter=DEFAULT_MAX_ITER) -> _lib.Problem:
+                 rtol=DEFAULT_RTOL, max_iter=DEFAULT_MAX_ITER, flags=0) -> _lib.Problem:
     return _lib.Problem(n=int(n), d=int(d), base=int(base), C=int(C), K=int(min(k, n)),
                         max_iter=int(max_iter), tau=float(tau), eps=_eps_value(epsilon),
-                        rtol=float(rtol), flags=0)
+                        rtol=float(rtol), flags=int(flags))
 
 
 def _stream(dev) -> int:

@@ -22,7 +22,7 @@ INCLUDE = os.path.join(ROOT, "include")
 OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libgll.so")
 ARCH = os.environ.get("GLL_OFFLOAD_ARCH", "gfx950")
-UNITS = ["knn.hip", "rows.hip", "solve.hip", "grad.hip", "api.hip"]
+UNITS = ["knn.hip", "rows.hip", "solve.hip", "gridcg.hip", "grad.hip", "api.hip"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
          "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
 

@@ -231,13 +231,23 @@ int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const f
                const float* b, float* x, float atol, int max_iter, int32_t* iters,
                int32_t* nonconv, void* workspace, void* stream) {
     if (m < 1 || C < 1 || !row_ptr || !col || !val || !b || !x) return GLL_ERR_INVALID_ARG;
+    if (m > 2048 && C <= 16) {   // whole-GPU cooperative CG (lanes per row from nnz ~ 8 m)
+        if (!workspace) return GLL_ERR_INVALID_ARG;
+        return hip_status(launch_cg_grid_csr(m, C, row_ptr, col, val, int64_t(m) * 8, b, x, atol,
+                                             max_iter > 0 ? max_iter : 100000, iters, nonconv,
+                                             static_cast<float*>(workspace),
+                                             static_cast<hipStream_t>(stream)));
+    }
     return hip_status(launch_cg_csr(m, C, row_ptr, col, val, b, x, atol,
                                     max_iter > 0 ? max_iter : 100000, iters, nonconv,
                                     static_cast<float*>(workspace),
                                     static_cast<hipStream_t>(stream)));
 }
 
-size_t gll_cg_csr_workspace_bytes(int m, int C) { return size_t(5) * m * C * sizeof(float); }
+size_t gll_cg_csr_workspace_bytes(int m, int C) {
+    const size_t per_col = size_t(5) * m * C, grid = grid_cg_workspace_floats(m, C);
+    return (per_col > grid ? per_col : grid) * sizeof(float);
+}
 
 int gll_prof_enable(int kid, int period) {
     if (kid < 0 || kid >= GLL_K_COUNT || period < 0) return GLL_ERR_INVALID_ARG;
@@ -294,6 +304,8 @@ void trace_read_knn(unsigned long long*);
 void trace_read_rows(unsigned long long*);
 void trace_read_solve(unsigned long long*);
 void trace_read_grad(unsigned long long*);
+void trace_read_gridcg(unsigned long long*);
+void trace_reset_gridcg();
 void trace_read_wg_knn(unsigned long long*);
 void trace_read_wg_solve(unsigned long long*);
 void trace_reset_knn();
@@ -309,6 +321,7 @@ extern "C" int gll_trace_read(int unit, unsigned long long* out) {
         case 1: gll::trace_read_rows(out); return GLL_OK;
         case 2: gll::trace_read_solve(out); return GLL_OK;
         case 3: gll::trace_read_grad(out); return GLL_OK;
+        case 4: gll::trace_read_gridcg(out); return GLL_OK;
         default: return GLL_ERR_INVALID_ARG;
     }
 }
@@ -329,6 +342,7 @@ extern "C" int gll_trace_reset(int unit) {
         case 1: gll::trace_reset_rows(); return GLL_OK;
         case 2: gll::trace_reset_solve(); return GLL_OK;
         case 3: gll::trace_reset_grad(); return GLL_OK;
+        case 4: gll::trace_reset_gridcg(); return GLL_OK;
         default: return GLL_ERR_INVALID_ARG;
     }
 }

@@ -106,8 +106,11 @@ inline int gram_splits(int n, int d) {
     return 1;
 }
 
+size_t grid_cg_workspace_floats(int m, int C);
+
 struct Layout {
     int n, d, base, m, C, K;
+    int flags;        // gll_problem.flags
     int KS;           // Gram split planes (gram_splits)
     int ldD;          // leading dimension of the n x n squared-distance matrix
     int RCAP;         // reverse-list capacity per row
@@ -118,6 +121,7 @@ struct Layout {
 
     explicit Layout(const gll_problem& p) {
         n = p.n; d = p.d; base = p.base; C = p.C;
+        flags = p.flags;
         K = p.K < p.n ? p.K : p.n;
         m = n - base;
         ldD = (n + 3) & ~3;
@@ -155,7 +159,9 @@ struct Layout {
         Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
         S = take(size_t(Etot) * 4);        // per-edge coefficient (auto eps only)
         b = take(size_t(n) * 4);           // auto-eps b_i (GLL.py:126)
-        cgv = take(size_t(5) * m * C * 4); // CG vectors when they do not fit in LDS
+        // CG vectors when they do not fit in LDS (per-column kernels) / of the grid-wide CG
+        const size_t gf = grid_cg_workspace_floats(m, C);
+        cgv = take((gf > size_t(5) * m * C ? gf : size_t(5) * m * C) * 4);
         total = off;
     }
     template <typename T>
@@ -345,6 +351,14 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
 hipError_t launch_cg_luu(const Layout& L, const Batch& bt, void* ws, const void* b,
                          size_t b_stride, int b_dtype, double* out64, float* out32, float rtol,
                          int max_iter, int32_t* st_nonconv, int32_t* st_iters, hipStream_t s);
+hipError_t launch_cg_grid_luu(const Layout& L, void* ws, const void* b, int b_dtype,
+                              double* out64, float* out32, float rtol, float atol,
+                              int max_iter, int32_t* st_nonconv, int32_t* st_iters,
+                              hipStream_t s);
+hipError_t launch_cg_grid_csr(int m, int C, const int32_t* row_ptr, const int32_t* col,
+                              const float* val, int64_t nnz, const float* b, float* x,
+                              float atol, int max_iter, int32_t* iters, int32_t* nonconv,
+                              float* ws, hipStream_t s);
 hipError_t launch_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col,
                          const float* val, const float* b, float* x, float atol, int max_iter,
                          int32_t* iters, int32_t* nonconv, float* gvec, hipStream_t s);

@@ -353,10 +353,14 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
                           double* out64, float* out32, float rtol, int max_iter,
                           int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
     size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4;
-    // entries past the ELL slices: at most (m + n)(K-1) U-block entries in all
+    // entries past the ELL slices (rare: hub rows) are compacted into LDS up to kOvfLds of
+    // them, the rest read from the CSR; capped so 4 workgroups still share a CU in batched
+    // launches (a full-LDS request would pin one per CU)
+    constexpr int64_t kOvfLds = 2048;
     const int64_t eu_bound = int64_t(L.m + L.n) * (L.K - 1);
     int64_t cap = int64_t(kLdsLimit - lds) / 8;
     if (cap > eu_bound) cap = eu_bound;
+    if (cap > kOvfLds) cap = kOvfLds;
     if (cap < 0) cap = 0;
     lds += size_t(cap) * 8;
     auto fn = cg_ell_kernel<NT, R, S, TB>;
@@ -374,6 +378,15 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
                               double* out64, float* out32, float rtol, int max_iter,
                               int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
     const int m = L.m;
+    // one persistent launch over the whole GPU (gridcg.hip) for a single graph past the
+    // per-column register kernels' sweet spot (m > 1024: their ELL slices overflow); measured
+    // at stress (m 4096, K 30): 209 us against 288 us per solve.  Batches keep the
+    // per-column kernels (B x C workgroups already fill the GPU).
+    if (bt.B == 1 && L.C <= 16 && (m > 1024 || (L.flags & GLL_FLAG_CG_GRID))) {
+        const int b_dtype = sizeof(TB) == 8 ? GLL_DT_F64 : GLL_DT_F32;
+        return launch_cg_grid_luu(L, ws, b, b_dtype, out64, out32, rtol, 0.f, max_iter,
+                                  st_nonconv, st_iters, s);
+    }
 #define GLL_ELL(NT, R, S)                                                                   \
     return run_ell<NT, R, S, TB>(L, bt, ws, b, bs, out64, out32, rtol, max_iter, st_nonconv, \
                                  st_iters, s)

@@ -41,6 +41,9 @@ extern "C" {
 #define GLL_ST_BWD_ITERS 4     /* max adjoint CG iterations over columns */
 #define GLL_ST_NWORDS 16
 
+/* gll_problem.flags */
+#define GLL_FLAG_CG_GRID 1   /* solve Luu with the grid-wide CG even when m <= 4096 */
+
 typedef struct gll_problem {
     int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */
     int32_t d;        /* feature dimension */
@@ -51,7 +54,7 @@ typedef struct gll_problem {
     float tau;        /* diagonal regulariser of Luu (GLL.py:48) */
     float eps;        /* > 0: fixed epsilon (GLL.py:226); <= 0: 'auto' (GLL.py:200-205) */
     float rtol;       /* CG stop: ||r_c|| <= rtol ||b_c|| per column; 0 => 1e-6 */
-    int32_t flags;    /* reserved, 0 */
+    int32_t flags;    /* GLL_FLAG_* bits, 0 by default */
     int32_t* status_sink; /* optional device words (GLL_ST_NWORDS): when non-NULL the public
                            * status words accumulate there across calls (sticky; the caller
                            * reads and clears them when it likes) instead of the workspace */
@@ -115,8 +118,9 @@ int gll_workspace_view(const gll_problem* p, void* workspace, gll_view* out);
  * Stops per column when ||r_c||_2 <= atol (absolute, like stable_conjgrad's tol) or
  * max_iter.  `iters` (device int, may be NULL) receives the max iteration count,
  * `nonconv` (device int, may be NULL) the columns that hit max_iter.  `workspace`
- * (gll_cg_csr_workspace_bytes, may be NULL when 5 m floats fit in LDS) holds the Krylov
- * vectors of large systems. */
+ * (gll_cg_csr_workspace_bytes) holds the Krylov vectors: required when m > 2048 (those
+ * systems run as one cooperative launch over the whole GPU, C <= 16), may be NULL when
+ * 5 m floats fit in LDS. */
 size_t gll_cg_csr_workspace_bytes(int m, int C);
 int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const float* val,
                const float* b, float* x, float atol, int max_iter, int32_t* iters,

@@ -323,3 +323,70 @@ def test_batched_shared_labels_python_and_cpp_paths_agree():
         ind = _gpu_knn(Xs[g], c["k"], 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
         Uo, _ = O.forward(Xs[g], Ys[0], tau=0.0, epsilon=1.0, K=c["k"], knn=(ind, None))
         assert O.rel_err(outs[0][0][g], Uo) <= TOL
+
+
+def _forward_c_abi(X, Y, k, tau, eps, flags=0):
+    """gll_forward through ctypes with explicit problem flags; returns (U, fwd iterations)."""
+    import ctypes as ct
+    from graphlearninglayer_amd import _lib
+    GLL = _gll()
+    n, d = X.shape
+    base, C = Y.shape
+    prob = GLL.make_problem(n, d, base, C, k, tau, eps, flags=flags)
+    lib = _lib.lib()
+    ws = torch.empty(lib.gll_workspace_bytes(ct.byref(prob)), dtype=torch.uint8, device="cuda")
+    U = torch.empty(n - base, C, dtype=torch.float64, device="cuda")
+    Xd = torch.from_numpy(np.ascontiguousarray(X)).cuda()
+    Yd = torch.from_numpy(np.ascontiguousarray(Y)).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.check(lib.gll_forward(ct.byref(prob), Xd.data_ptr(), Yd.data_ptr(), _lib.GLL_DT_F32,
+                               ws.data_ptr(), U.data_ptr(), s), "gll_forward")
+    st = ws[: 4 * _lib.ST_NWORDS].view(torch.int32).cpu().tolist()
+    return U.cpu().numpy(), st[_lib.ST_FWD_ITERS], st[_lib.ST_FWD_NONCONV]
+
+
+def test_grid_cg_forced_at_ns_matches_oracle():
+    """The whole-GPU cooperative CG (gridcg.hip) on the NS graph vs the float64 oracle."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import CONFIGS, one_hot, synth
+    c = CONFIGS["ns"]
+    X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=0)
+    Y = one_hot(lab[: c["base"]])
+    Ug, itg, ncg = _forward_c_abi(X, Y, c["k"], 0.07, 1.0, flags=_lib.FLAG_CG_GRID)
+    Ue, ite, nce = _forward_c_abi(X, Y, c["k"], 0.07, 1.0)
+    assert ncg == 0 and nce == 0 and 0 < itg <= ite + 2
+    ind = _gpu_knn(X, c["k"], 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, _ = O.forward(X, Y, tau=0.07, epsilon=1.0, K=c["k"], knn=(ind, None))
+    assert O.rel_err(Ug, Uo) <= TOL
+    assert O.rel_err(Ug, Ue) <= 1e-5
+
+
+def test_grid_cg_large_system_fwd_bwd_matches_oracle():
+    """m = 6000 > 4096 selects the grid CG automatically (forward and adjoint)."""
+    from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
+    base, m, d, k = 2000, 6000, 64, 10
+    X, lab = synth(base, m, d, r=1.0, seed=5)
+    Y = one_hot(lab[:base])
+    g = seeded_gbar(m, 10, 7)
+    U, grad = _run(X, Y, 0.07, 1.0, k, g)
+    ind = _gpu_knn(X, k, 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, st = O.forward(X, Y, tau=0.07, epsilon=1.0, K=k, knn=(ind, None))
+    go = O.backward(st, g)
+    assert O.rel_err(U, Uo) <= TOL
+    assert O.rel_err(grad, go) <= TOL
+
+
+def test_cg_csr_large_matches_scipy():
+    """gll_cg_csr for m > 2048 (grid CG) against a direct sparse solve."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    GLL = _gll()
+    rng = np.random.default_rng(3)
+    m, C = 5000, 4
+    A = sp.random(m, m, density=6.0 / m, random_state=rng, format="csr")
+    A = A + A.T
+    A = (sp.diags(np.asarray(abs(A).sum(1)).ravel() + 0.5) + A).tocsr()   # SPD, dominant
+    b = rng.standard_normal((m, C))
+    x = GLL.stable_conjgrad(A, b, tol=1e-8)
+    xe = spla.spsolve(A.tocsc(), b)
+    assert np.max(np.abs(x - xe)) <= 1e-6 * np.max(np.abs(xe))
