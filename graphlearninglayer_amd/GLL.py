@@ -332,6 +332,49 @@ def knn_sym_dist(data, k=DEFAULT_K, epsilon="auto"):
 # ----------------------------------------------------------------------------------------
 # stable_conjgrad: device multi-RHS CG
 # ----------------------------------------------------------------------------------------
+def refined_solve(rp, ci, val64, B, x=None, tol=1e-10, max_iter=100000, weight=None):
+    """Solve A x = B (A SPD, device CSR: int32 row_ptr / col, float64 values; B m x C float64)
+    to max_c ||weight * (B - A x)_c||_2 <= tol.
+
+    fp32 Jacobi-CG corrections (libgll gll_cg_csr: the whole-GPU CG for m > 2048) inside
+    float64 iterative refinement; the float64 residual uses torch sparse on the GPU.
+    Returns (x, err, CG iterations)."""
+    dev = B.device
+    m, C = B.shape
+    val32 = val64.float().contiguous()
+    with warnings.catch_warnings():   # "sparse CSR support is in beta" (torch 2.10)
+        warnings.simplefilter("ignore", UserWarning)
+        A64 = torch.sparse_csr_tensor(rp.long(), ci.long(), val64, size=(m, m))
+    x = torch.zeros_like(B) if x is None else x
+    ws = torch.empty(_lib.lib().gll_cg_csr_workspace_bytes(m, C), dtype=torch.uint8, device=dev)
+    counters = torch.zeros(2, dtype=torch.int32, device=dev)
+    total = 0
+    max_iter = int(max_iter)
+
+    def residual(x):
+        r = B - (A64 @ x)
+        rw = r if weight is None else r * weight[:, None]
+        return r, torch.linalg.vector_norm(rw, dim=0).max().item()
+
+    r, err = residual(x)
+    for _ in range(32):  # refinement sweeps
+        if err <= tol or total >= max_iter:
+            break
+        scale = max(torch.linalg.vector_norm(r, dim=0).max().item(), 1e-300)
+        r32 = (r / scale).float().contiguous()
+        d32 = torch.empty_like(r32)
+        counters.zero_()
+        _lib.check(_lib.lib().gll_cg_csr(m, C, rp.data_ptr(), ci.data_ptr(), val32.data_ptr(),
+                                         r32.data_ptr(), d32.data_ptr(),
+                                         ct.c_float(1e-6), max_iter - total,
+                                         counters.data_ptr(), counters[1:].data_ptr(),
+                                         ws.data_ptr(), _stream(dev)), "gll_cg_csr")
+        total += int(counters[0].item())
+        x = x + scale * d32.double()
+        r, err = residual(x)
+    return x, err, total
+
+
 def stable_conjgrad(A, b, x0=None, max_iter=1e5, tol=1e-10):
     """Mirror of GLL.py:247-276: solve A x = b (A SPD, b n x C) to max_col ||r||_2 <= tol.
 
@@ -351,32 +394,9 @@ def stable_conjgrad(A, b, x0=None, max_iter=1e5, tol=1e-10):
     rp = torch.from_numpy(A.indptr.astype(np.int32)).to(dev)
     ci = torch.from_numpy(A.indices.astype(np.int32)).to(dev)
     val64 = torch.from_numpy(A.data.astype(np.float64)).to(dev)
-    val32 = val64.float()
-    A64 = torch.sparse_csr_tensor(rp.long(), ci.long(), val64, size=(m, m))
-    x = torch.zeros_like(B) if x0 is None else torch.from_numpy(
+    x = None if x0 is None else torch.from_numpy(
         np.asarray(x0, dtype=np.float64).reshape(m, C)).to(dev)
-    ws = torch.empty(_lib.lib().gll_cg_csr_workspace_bytes(m, C), dtype=torch.uint8, device=dev)
-    counters = torch.zeros(2, dtype=torch.int32, device=dev)
-    total = 0
-    max_iter = int(max_iter)
-    for _ in range(32):  # refinement sweeps
-        r = B - (A64 @ x)
-        err = torch.linalg.vector_norm(r, dim=0).max().item()
-        if err <= tol or total >= max_iter:
-            break
-        scale = max(err, 1e-300)
-        r32 = (r / scale).float().contiguous()
-        d32 = torch.empty_like(r32)
-        counters.zero_()
-        _lib.check(_lib.lib().gll_cg_csr(m, C, rp.data_ptr(), ci.data_ptr(), val32.data_ptr(),
-                                         r32.data_ptr(), d32.data_ptr(),
-                                         ct.c_float(1e-6), max_iter - total,
-                                         counters.data_ptr(), counters[1:].data_ptr(),
-                                         ws.data_ptr(), _stream(dev)), "gll_cg_csr")
-        total += int(counters[0].item())
-        x = x + scale * d32.double()
-    else:
-        err = torch.linalg.vector_norm(B - A64 @ x, dim=0).max().item()
+    x, err, total = refined_solve(rp, ci, val64, B, x, tol, max_iter)
     if err > tol:
         print("max iter reached: ", total, " iters")  # GLL.py:273-274
     out = x.cpu().numpy()

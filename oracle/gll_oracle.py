@@ -169,3 +169,40 @@ def rel_err(a, b) -> float:
     b = np.asarray(b, dtype=np.float64)
     den = np.max(np.abs(b))
     return float(np.max(np.abs(a - b)) / (den if den > 0 else 1.0))
+
+
+# ----------------------------------------------------------------------------------------
+# utils.laplace: the large single-graph evaluation path
+# ----------------------------------------------------------------------------------------
+def one_hot_encode(labels, n_classes="auto"):
+    """utils.py:556-568: labels -> n_labels x C one-hot, C = #unique labels when 'auto'."""
+    labels = np.asarray(labels)
+    C = len(np.unique(labels)) if n_classes == "auto" else int(n_classes)
+    Y = np.zeros((len(labels), C))
+    Y[np.arange(len(labels)), labels] = 1
+    return Y
+
+
+def laplace(X, train_labels, knn_num=50, epsilon="auto", n_classes="auto", tau=1e-8, knn=None):
+    """utils.py:570-593 in closed form: W from the symmetrised kNN graph (knn_sym_dist), L =
+    D - W (csgraph.laplacian, utils.py:575), Luu = L[k:,k:] + tau I, rhs = -Lul Y; the
+    reference solves the Jacobi-scaled system (M Luu M) y = M rhs with stable_conjgrad to
+    1e-10 and returns M y (utils.py:585-592) -- mathematically Luu^{-1} rhs, solved here
+    directly (SuperLU).  `knn` = (ind, dist) overrides the exact search."""
+    X = np.asarray(X, dtype=np.float64)
+    Y = one_hot_encode(train_labels, n_classes)
+    k = Y.shape[0]
+    if knn is None:
+        ind, dist = knn_exact(X, knn_num)
+    else:
+        ind, dist = knn
+        if dist is None:
+            dist = np.sqrt(((X[:, None, :] - X[np.asarray(ind)]) ** 2).sum(-1))
+    g = graph_from_knn(ind, dist, epsilon)
+    W = g.csr(g.W)
+    deg = np.asarray(W.sum(axis=0)).ravel()
+    L = (sparse.diags(deg) - W).tocsr()
+    m = g.n - k
+    Luu = (L[k:, k:] + tau * sparse.eye(m)).tocsc()
+    rhs = -(L[k:, :k] @ Y)
+    return spla.spsolve(Luu, rhs).reshape(m, -1)

@@ -116,9 +116,44 @@ def run_case(mod, cfg, eps, tau, ydt):
     return out
 
 
+# utils.laplace (utils.py:570-593) can not be imported here (utils.py needs torchvision and
+# the networks package); its body is glue around the reference GLL functions, so the fixture
+# is produced by the REFERENCE knn_sym_dist and stable_conjgrad driven by that glue,
+# restated step by step below with utils.py line numbers.
+LAPLACE = dict(labeled=250, unlabeled=2750, d=64, knn_num=50, epsilon=1.0, tau=1e-8, r=1.0,
+               seed=21)
+
+
+def run_laplace(mod):
+    import scipy.sparse as sparse
+    from oracle.gll_oracle import one_hot_encode
+
+    p = LAPLACE
+    X, labels = synth(p["labeled"], p["unlabeled"], p["d"], C=10, r=p["r"], seed=p["seed"])
+    train = labels[: p["labeled"]]
+    W, _, _, _, knn = mod.knn_sym_dist(X, k=p["knn_num"], epsilon=p["epsilon"])   # utils.py:574
+    L = sparse.csgraph.laplacian(W).tocsr()                                        # utils.py:575
+    Y = one_hot_encode(train, "auto")                                              # utils.py:576
+    k = Y.shape[0]                                                                 # utils.py:577
+    Luu, Lul = L[k:, k:], L[k:, :k]                                                # utils.py:579-580
+    m = Luu.shape[0]
+    Luu = Luu + sparse.spdiags(p["tau"] * np.ones(m), 0, m, m).tocsr()             # utils.py:584
+    M = Luu.diagonal()                                                             # utils.py:586
+    M = sparse.spdiags(1 / np.sqrt(M + 1e-10), 0, m, m).tocsr()                    # utils.py:587
+    pred = mod.stable_conjgrad(M * Luu * M, -M * Lul @ Y)                          # utils.py:589-590
+    pred = M * pred                                                                # utils.py:591
+    meta = dict(LAPLACE, x_sha256=sha256(X), C=10)
+    return dict(meta=json.dumps(meta), U=np.asarray(pred),
+                knn=np.asarray(knn).astype(np.int16), labels=labels.astype(np.int16))
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     mod = load_reference()
+    lap = run_laplace(mod)
+    path = os.path.join(HERE, "laplace_small.npz")
+    np.savez_compressed(path, **lap)
+    print(f"laplace_small: U max {np.abs(lap['U']).max():.4g} -> {os.path.getsize(path)/1024:.0f} KB")
     for cfg, eps, tau, ydt in CASES:
         name = case_name(cfg, eps, tau, ydt)
         out = run_case(mod, cfg, eps, tau, ydt)

@@ -390,3 +390,41 @@ def test_cg_csr_large_matches_scipy():
     x = GLL.stable_conjgrad(A, b, tol=1e-8)
     xe = spla.spsolve(A.tocsc(), b)
     assert np.max(np.abs(x - xe)) <= 1e-6 * np.max(np.abs(xe))
+
+
+def test_utils_laplace_matches_reference_fixture():
+    """utils.laplace on the GPU vs the reference pipeline's fixture."""
+    import json
+    import os
+    from graphlearninglayer_amd import utils as U_
+    from graphlearninglayer_amd.synth import synth
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                             "laplace_small.npz"))
+    p = json.loads(str(z["meta"]))
+    X, labels = synth(p["labeled"], p["unlabeled"], p["d"], C=10, r=p["r"], seed=p["seed"])
+    train = labels[: p["labeled"]]
+    U = U_.laplace(X, train, knn_num=p["knn_num"], epsilon=p["epsilon"], tau=p["tau"])
+    assert U.shape == z["U"].shape and U.dtype == np.float64
+    ind = _gpu_knn(X, p["knn_num"], p["epsilon"])["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo = O.laplace(X, train, knn_num=p["knn_num"], epsilon=p["epsilon"], tau=p["tau"],
+                   knn=(ind, None))
+    assert O.rel_err(U, Uo) <= TOL
+    assert len(O.knn_set_mismatch(X, ind, p["knn_num"])) == 0   # only near-ties may differ
+    ref_ind = z["knn"].astype(np.int64)
+    if all(set(a) == set(b) for a, b in zip(ind.tolist(), ref_ind.tolist())):
+        assert O.rel_err(U, z["U"]) <= TOL
+    assert np.mean(U.argmax(1) == z["U"].argmax(1)) >= 0.999
+
+
+def test_utils_laplace_large_graph_matches_oracle():
+    """n = 20,250 (250 labeled), d = 128, k = 50: the whole-GPU CG + float64 refinement."""
+    from graphlearninglayer_amd import utils as U_
+    from graphlearninglayer_amd.synth import synth
+    X, labels = synth(250, 20000, 128, C=10, r=1.0, seed=8)
+    train = labels[:250]
+    U = U_.laplace(X, train, knn_num=50, epsilon=1.0, tau=1e-8)
+    ind = _gpu_knn(X, 50, 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo = O.laplace(X, train, knn_num=50, epsilon=1.0, tau=1e-8, knn=(ind, None))
+    assert O.rel_err(U, Uo) <= TOL
+    acc = U_.gl_accuracy(X[:250], train, X[250:], labels[250:])
+    assert acc == pytest.approx(100.0 * np.mean(Uo.argmax(1) == labels[250:]), abs=0.05)

@@ -1,6 +1,8 @@
 """The oracle restatements against fixtures produced by the reference GLL.py itself.
 
 This pins the oracle before it is trusted as the checker of the HIP path (CPU only)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -8,6 +10,8 @@ import torch
 from oracle import gll_oracle as O
 from oracle import gll_port as PT
 from tests.golden_io import Case, names
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 CASES = names()
 
@@ -64,3 +68,18 @@ def test_fd_gradient_plumbing():
     fd = np.sum((Up - Um) * c.gbar) / (2 * h)
     an = np.sum(g * D)
     assert abs(fd - an) / abs(an) < 1e-6
+
+
+def test_oracle_laplace_matches_reference_fixture():
+    """utils.laplace: the closed-form oracle vs the reference pipeline
+    (reference knn_sym_dist + stable_conjgrad driven by utils.py:570-593's glue)."""
+    import json
+    from graphlearninglayer_amd.synth import sha256, synth
+    z = np.load(os.path.join(GOLDEN, "laplace_small.npz"))
+    p = json.loads(str(z["meta"]))
+    X, labels = synth(p["labeled"], p["unlabeled"], p["d"], C=10, r=p["r"], seed=p["seed"])
+    assert sha256(X) == p["x_sha256"]
+    np.testing.assert_array_equal(labels, z["labels"])
+    U = O.laplace(X, labels[: p["labeled"]], knn_num=p["knn_num"], epsilon=p["epsilon"],
+                  tau=p["tau"])
+    assert O.rel_err(U, z["U"]) <= 1e-9
