@@ -26,6 +26,12 @@ constexpr int kWave = 64;
 constexpr int kStOvfCount = 8;   // internal status words: overflow-list length
 constexpr int kStBump = 9;       //                        bump-region cursor
 
+// ELL slice width of the per-column CG kernels for m unlabeled rows (solve.hip dispatch);
+// row_build emits that many column-major (col, w) slots per U row, 0 when no ELL kernel runs.
+inline int ell_slots(int m) {
+    return m <= 512 ? 24 : (m <= 1024 ? 16 : (m <= 2048 ? 8 : (m <= 4096 ? 4 : 0)));
+}
+
 // ---------------------------------------------------------------------------------------
 // In-kernel timestamps (diagnostic builds only: build.py --trace defines GLL_TRACE and
 // writes libgll_trace.so; the product library compiles these to nothing).  Per translation
@@ -118,6 +124,8 @@ struct Layout {
     int64_t Etot;     // entry capacity: n Wcap slots + 2 n (K-1) bump region
     size_t status, D2, knn_idx, knn_d2, eps, rev_cnt, rev_idx, rev_d2, ovf, row_start, row_len;
     size_t tmp_col, tmp_d2, col, w, d2e, deg, ucnt, diag, rhs, P, Wadj, S, b, cgv, total;
+    int SE;           // ELL slots per U row (ell_slots)
+    size_t ell_col, ell_w;
 
     explicit Layout(const gll_problem& p) {
         n = p.n; d = p.d; base = p.base; C = p.C;
@@ -155,6 +163,9 @@ struct Layout {
         ucnt = take(size_t(m) * 4);        // U-block entries per unlabeled row
         diag = take(size_t(m) * 4);
         rhs = take(size_t(m) * C * 4);
+        SE = ell_slots(m);
+        ell_col = take(size_t(SE) * m * 4);   // [SE][m] U-block columns (U index), 0-padded
+        ell_w = take(size_t(SE) * m * 4);     // [SE][m] weights W_uj, 0-padded
         P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)
         Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
         S = take(size_t(Etot) * 4);        // per-edge coefficient (auto eps only)

@@ -47,6 +47,9 @@ struct RowArgs {
     float* rhs;
     float* P;
     float* Wadj;
+    int32_t* ell_col;   // [SE][m] column-major U slices for the CG (SE = 0: none)
+    float* ell_w;
+    int SE, m;
     size_t wss;   // batched launches: workspace stride between graphs (bytes)
 
     __device__ void to_graph() {   // move every workspace pointer to graph blockIdx.y
@@ -71,6 +74,8 @@ struct RowArgs {
         rhs = gshift(rhs, wss);
         P = gshift(P, wss);
         Wadj = gshift(Wadj, wss);
+        ell_col = gshift(ell_col, wss);
+        ell_w = gshift(ell_w, wss);
     }
 };
 
@@ -174,6 +179,17 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
     float racc[kMaxCPerLane];
 #pragma unroll
     for (int q = 0; q < kMaxCPerLane; ++q) racc[q] = 0.f;
+    if (i >= a.base && a.SE > 0) {   // column-major ELL slice of the U block for the CG
+        const int u = i - a.base, nu = L - nlab;
+        if (lane < a.SE) {
+            const bool live = lane < nu;
+            const int e = nlab + (live ? lane : 0);
+            const int c = live ? ocol[e] - a.base : 0;
+            const float we = live ? ow[e] : 0.f;
+            a.ell_col[size_t(lane) * a.m + u] = c;
+            a.ell_w[size_t(lane) * a.m + u] = we;
+        }
+    }
     if (i >= a.base) {
         for (int e = 0; e < nlab; ++e) {
             const int j = ocol[e];
@@ -282,6 +298,10 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     a.rhs = L.at<float>(ws, L.rhs);
     a.P = L.at<float>(ws, L.P);
     a.Wadj = L.at<float>(ws, L.Wadj);
+    a.ell_col = L.at<int32_t>(ws, L.ell_col);
+    a.ell_w = L.at<float>(ws, L.ell_w);
+    a.SE = L.SE;
+    a.m = L.m;
     a.wss = bt.ws;
     dim3 grid((L.n + 3) / 4, bt.B);
     prof_begin(GLL_K_FINALIZE, s);

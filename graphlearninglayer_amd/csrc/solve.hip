@@ -101,8 +101,12 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     const int32_t* __restrict__ col, const float* __restrict__ wv, const float* __restrict__ diag,
     const TB* __restrict__ bsrc, double* __restrict__ out64, float* __restrict__ out32,
     float rtol, int max_iter, int mat_cap, int32_t* __restrict__ st_nonconv,
-    int32_t* __restrict__ st_iters, size_t wss, size_t bs, size_t us, size_t sts) {
+    int32_t* __restrict__ st_iters, const int32_t* __restrict__ ell_col,
+    const float* __restrict__ ell_w, size_t wss, size_t bs,
+    size_t us, size_t sts) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
+    ell_col = gshift(ell_col, wss);
+    ell_w = gshift(ell_w, wss);
     row_start = gshift(row_start, wss);   // batched launches: graph blockIdx.y
     row_len = gshift(row_len, wss);
     ucnt = gshift(ucnt, wss);
@@ -129,27 +133,35 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     int tov = 0;
     GLL_TRACE_SCOPE(0);
     GLL_TRACE_PT(0);
+    // entries past the S ELL slots exist only when some U block is longer than S: one
+    // workgroup-wide OR (a single barrier) decides, so the usual case skips the overflow scan
+    int longer = 0;
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int u = tid + NT * q;
-        int len = 0, st = 0;
-        x[q] = r[q] = p[q] = ap[q] = mi[q] = dg[q] = 0.f;
-        if (u < m) {
-            len = ucnt[u];   // U block = sorted suffix of graph row base + u
-            st = row_start[base + u] + row_len[base + u] - len;
-        }
+        longer |= (u < m && ucnt[u] > S) ? 1 : 0;
+    }
+    const bool has_ovf = __syncthreads_or(longer) != 0;
 #pragma unroll
-        for (int s = 0; s < S; ++s) {   // ELL slice: independent loads, padded with (0, 0)
-            const bool live = s < len;
-            const int e = live ? st + s : 0;
-            const int cc = col[e] - base;
-            const float ww = wv[e];
-            ec[q][s] = live ? cc : 0;
-            ew[q][s] = live ? ww : 0.f;
+    for (int q = 0; q < R; ++q) {
+        const int u = tid + NT * q;
+        const int uc = u < m ? u : 0;
+        x[q] = r[q] = p[q] = ap[q] = mi[q] = dg[q] = 0.f;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {   // column-major ELL slices (row_build): coalesced, padded
+            const int cc = ell_col[size_t(s) * m + uc];
+            const float ww = ell_w[size_t(s) * m + uc];
+            ec[q][s] = u < m ? cc : 0;
+            ew[q][s] = u < m ? ww : 0.f;
         }
-        ost[q] = st + S;
-        olen[q] = len - S;
-        tov += olen[q] > 0 ? olen[q] : 0;
+        ost[q] = 0;
+        olen[q] = 0;
+        if (has_ovf && u < m) {
+            const int len = ucnt[u];   // U block = sorted suffix of graph row base + u
+            ost[q] = row_start[base + u] + row_len[base + u] - len + S;
+            olen[q] = len - S;
+            tov += olen[q] > 0 ? olen[q] : 0;
+        }
         if (u < m) {
             dg[q] = diag[u];
             mi[q] = dg[q] > 0.f ? 1.f / dg[q] : 0.f;
@@ -164,9 +176,9 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     GLL_TRACE_PT(1);
     // entries beyond the ELL slices: compact them into LDS when they fit
     int ov_total = 0;
-    int ooff = block_excl_scan<NT>(tov, scan, ov_total);
+    int ooff = has_ovf ? block_excl_scan<NT>(tov, scan, ov_total) : 0;
     const bool matl = ov_total <= mat_cap;
-    if (matl) {
+    if (has_ovf && matl) {
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             for (int t = 0; t < olen[q]; ++t) {
@@ -363,13 +375,14 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
     if (cap > kOvfLds) cap = kOvfLds;
     if (cap < 0) cap = 0;
     lds += size_t(cap) * 8;
+    if (S != L.SE) return hipErrorInvalidValue;   // row_build emitted L.SE slots
     auto fn = cg_ell_kernel<NT, R, S, TB>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
     fn<<<dim3(L.C, bt.B), NT, lds, s>>>(
         L.m, L.C, L.base, L.at<int32_t>(ws, L.row_start), L.at<int32_t>(ws, L.row_len),
         L.at<int32_t>(ws, L.ucnt), L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
         L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, int(cap), st_nonconv, st_iters,
-        bt.ws, bs, bt.u, bt.st);
+        L.at<int32_t>(ws, L.ell_col), L.at<float>(ws, L.ell_w), bt.ws, bs, bt.u, bt.st);
     return hipGetLastError();
 }
 
