@@ -4,6 +4,8 @@
 // stream.  No allocation, no host synchronisation: the caller owns the workspace (the
 // Python mirror takes it from torch's caching allocator) and keeps it alive from
 // gll_forward to gll_backward, as the reference keeps its graph on ctx (GLL.py:69-70).
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -61,6 +63,13 @@ void prof_end(int kid, hipStream_t s) {
     }
     (void)hipEventRecord(e, s);
     g_prof.pending[kid].push_back(e);
+}
+
+hipError_t launch_status(const char* what) {
+    const hipError_t e = hipGetLastError();
+    static const bool dbg = getenv("GLL_DEBUG") != nullptr;
+    if (e != hipSuccess && dbg) fprintf(stderr, "gll: %s: %s\n", what, hipGetErrorString(e));
+    return e;
 }
 
 static const char* kKernelNames[GLL_K_COUNT] = {

@@ -345,6 +345,9 @@ __device__ __forceinline__ T* gshift(T* p, size_t stride) {
     return reinterpret_cast<T*>(reinterpret_cast<B*>(p) + size_t(blockIdx.y) * stride);
 }
 
+// Launch-error report (GLL_DEBUG=1 in the environment): which launcher failed and why.
+hipError_t launch_status(const char* what);
+
 // ---------------------------------------------------------------------------------------
 // Launchers (host side, one per translation unit)
 // ---------------------------------------------------------------------------------------

@@ -177,7 +177,7 @@ static hipError_t grad_nd(const EdgeArgs& a, const Batch& bt, const float* X, fl
     else if (nd <= 16) GLL_GRAD(16);
     else return hipErrorInvalidValue;
 #undef GLL_GRAD
-    return hipGetLastError();
+    return launch_status("grad.hip:grad_nd");
 }
 
 hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, const float* X,

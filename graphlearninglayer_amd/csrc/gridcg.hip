@@ -429,7 +429,7 @@ static hipError_t launch_grid(const Mat& A, GridCgArgs a, int G, float* ws, hipS
     hipError_t e = hipMemsetAsync(a.sync, 0, 16, s);
     if (e != hipSuccess) return e;
     cg_grid_kernel<Mat, LPR, RPG><<<dim3(unsigned(G)), kGT, 0, s>>>(A, a);
-    return hipGetLastError();
+    return launch_status("gridcg.hip:launch_grid");
 }
 
 // Lanes per row from the mean row length; rows per lane group (registers) and workgroups:

@@ -40,8 +40,9 @@ GLL_TRACE_UNIT(knn)
 // super-chunk is loaded into ring slot c right after slot c went to LDS, so a load has
 // NCH-1 chunks of MFMA work to hide behind; LDS is double-buffered per chunk.
 // --------------------------------------------------------------------------------------
-constexpr int kGK = 64;         // k per LDS chunk
-constexpr int kGL = kGK + 4;    // padded LDS row (floats): conflict-free ds_read_b128
+// k per LDS chunk: GK = 64 or 128 (template); rows padded to GK + 4 floats (conflict-free
+// ds_read_b128).  128-deep chunks halve the barriers per tile (one LDS turnaround each).
+constexpr int kGK = 64;
 
 // 16 MFMAs over 32 k: lane (r, h) holds A[r][8u + 4h + t], B[c=r][8u + 4h + t]
 __device__ __forceinline__ void gram_chunk_mfma(const f32x4 (&a)[4], const f32x4 (&b)[4],
@@ -57,7 +58,7 @@ __device__ __forceinline__ void gram_chunk_mfma(const f32x4 (&a)[4], const f32x4
     }
 }
 
-template <bool VEC, int NCH>
+template <bool VEC, int NCH, int GK>
 __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__ X, int n, int d,
                                                        int T, int KS, int kspan,
                                                        float* __restrict__ D2, int ld,
@@ -70,6 +71,8 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
     D2 = gshift(D2, wss);
     status = gshift(status, wss);
     rev_cnt = gshift(rev_cnt, wss);
+    constexpr int kGL = GK + 4;
+    constexpr int CS = GK / 64;   // 64-column segments of a chunk row
     // stage[buf][A|B][64 rows][kGL]; the epilogue reuses the same storage
     __shared__ __attribute__((aligned(16))) float smem[2 * 2 * 64 * kGL];
     __shared__ float s_sq[2][64];
@@ -94,7 +97,7 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
     GLL_TRACE_PT(10);
     const int k_lo = ks * kspan;
     const int k_hi = min(d, k_lo + kspan);
-    const int nsup = kspan / (kGK * NCH);
+    const int nsup = kspan / (GK * NCH);
     // loader role: thread t moves float4 column 4 (t & 15) of rows (t >> 4) and (t >> 4) + 32
     // of A and of B for every chunk
     const int lrow = tid >> 4, lcol = 4 * (tid & 15);
@@ -102,22 +105,29 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
     const float* ga1 = X + size_t(min(bi * 64 + lrow + 32, n - 1)) * d;
     const float* gb0 = X + size_t(min(bj * 64 + lrow, n - 1)) * d;
     const float* gb1 = X + size_t(min(bj * 64 + lrow + 32, n - 1)) * d;
-    f32x4 ring[NCH][4];
-    auto gload = [&](int chunk, f32x4 (&v)[4]) {   // raw: masked when stored to LDS
-        const int k = k_lo + chunk * kGK + lcol;
-        v[0] = load4_raw<VEC>(ga0, k, k_hi);
-        v[1] = load4_raw<VEC>(ga1, k, k_hi);
-        v[2] = load4_raw<VEC>(gb0, k, k_hi);
-        v[3] = load4_raw<VEC>(gb1, k, k_hi);
+    f32x4 ring[NCH][4 * CS];
+    auto gload = [&](int chunk, f32x4 (&v)[4 * CS]) {   // raw: masked when stored to LDS
+#pragma unroll
+        for (int cs = 0; cs < CS; ++cs) {
+            const int k = k_lo + chunk * GK + cs * 64 + lcol;
+            v[4 * cs + 0] = load4_raw<VEC>(ga0, k, k_hi);
+            v[4 * cs + 1] = load4_raw<VEC>(ga1, k, k_hi);
+            v[4 * cs + 2] = load4_raw<VEC>(gb0, k, k_hi);
+            v[4 * cs + 3] = load4_raw<VEC>(gb1, k, k_hi);
+        }
     };
-    auto lstore = [&](int chunk, int buf, const f32x4 (&v)[4]) {
-        const int k = k_lo + chunk * kGK + lcol;
+    auto lstore = [&](int chunk, int buf, const f32x4 (&v)[4 * CS]) {
         float* A = smem + (buf * 2 + 0) * 64 * kGL;
         float* B = smem + (buf * 2 + 1) * 64 * kGL;
-        *reinterpret_cast<f32x4*>(A + lrow * kGL + lcol) = mask4<VEC>(v[0], k, k_hi);
-        *reinterpret_cast<f32x4*>(A + (lrow + 32) * kGL + lcol) = mask4<VEC>(v[1], k, k_hi);
-        *reinterpret_cast<f32x4*>(B + lrow * kGL + lcol) = mask4<VEC>(v[2], k, k_hi);
-        *reinterpret_cast<f32x4*>(B + (lrow + 32) * kGL + lcol) = mask4<VEC>(v[3], k, k_hi);
+#pragma unroll
+        for (int cs = 0; cs < CS; ++cs) {
+            const int k = k_lo + chunk * GK + cs * 64 + lcol;
+            const int col = cs * 64 + lcol;
+            *reinterpret_cast<f32x4*>(A + lrow * kGL + col) = mask4<VEC>(v[4 * cs + 0], k, k_hi);
+            *reinterpret_cast<f32x4*>(A + (lrow + 32) * kGL + col) = mask4<VEC>(v[4 * cs + 1], k, k_hi);
+            *reinterpret_cast<f32x4*>(B + lrow * kGL + col) = mask4<VEC>(v[4 * cs + 2], k, k_hi);
+            *reinterpret_cast<f32x4*>(B + (lrow + 32) * kGL + col) = mask4<VEC>(v[4 * cs + 3], k, k_hi);
+        }
     };
     f32x16 acc;
 #pragma unroll
@@ -138,15 +148,20 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
             if constexpr (decltype(reload)::value) gload(min(sc + 1, nsup - 1) * NCH + c, ring[c]);
             __syncthreads();
             if (sc == 0 && c == 0) GLL_TRACE_PT(15);
-            const float* A = smem + (buf * 2 + 0) * 64 * kGL + arow * kGL + kh * 32 + 4 * h;
-            const float* B = smem + (buf * 2 + 1) * 64 * kGL + brow * kGL + kh * 32 + 4 * h;
-            f32x4 a[4], b[4];
+            // wave half kh takes k [kh GK/2, (kh+1) GK/2) of the chunk, 32 at a time
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                a[u] = *reinterpret_cast<const f32x4*>(A + 8 * u);
-                b[u] = *reinterpret_cast<const f32x4*>(B + 8 * u);
+            for (int sub = 0; sub < CS; ++sub) {
+                const int ko = kh * (GK / 2) + sub * 32 + 4 * h;
+                const float* A = smem + (buf * 2 + 0) * 64 * kGL + arow * kGL + ko;
+                const float* B = smem + (buf * 2 + 1) * 64 * kGL + brow * kGL + ko;
+                f32x4 a[4], b[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    a[u] = *reinterpret_cast<const f32x4*>(A + 8 * u);
+                    b[u] = *reinterpret_cast<const f32x4*>(B + 8 * u);
+                }
+                gram_chunk_mfma(a, b, acc, sa, sb);
             }
-            gram_chunk_mfma(a, b, acc, sa, sb);
         }
     };
     if (nsup == 1) {
@@ -463,27 +478,31 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
     const int T = (L.n + 63) / 64;
     const int tiles = T * (T + 1) / 2;
     const int KS = L.KS;
-    // slice of the features per split, in whole 64-deep chunks, grouped NCH per super-chunk
-    int kspan = ((L.d + KS - 1) / KS + kGK - 1) / kGK * kGK;
-    const int NCH = kspan >= 4 * kGK ? 4 : (kspan >= 2 * kGK ? 2 : 1);
-    kspan = (kspan + NCH * kGK - 1) / (NCH * kGK) * (NCH * kGK);
+    // slice of the features per split in whole 64-deep chunks, grouped NCH per super-chunk.
+    // (128-deep chunks -- half the barriers -- measured no faster at NS, B = 64 or stress:
+    // profiles/r01_gram_chunk_depth.txt; the template keeps the depth a parameter.)
+    constexpr int GK = kGK;
+    const int dsl = (L.d + KS - 1) / KS;
+    int kspan = (dsl + GK - 1) / GK * GK;
+    const int NCH = kspan >= 4 * GK ? 4 : (kspan >= 2 * GK ? 2 : 1);
+    kspan = (kspan + NCH * GK - 1) / (NCH * GK) * (NCH * GK);
     float* D2 = L.at<float>(ws, L.D2);
     const size_t plane = size_t(L.n) * L.ldD;
     int32_t* st = L.at<int32_t>(ws, L.status);
     int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
     const dim3 grid(tiles * KS, bt.B);
     prof_begin(GLL_K_GRAM, s);
-#define GLL_GRAM(V, N) \
-    gram_lds_kernel<V, N><<<grid, 512, 0, s>>>(X, L.n, L.d, T, KS, kspan, D2, L.ldD, plane, st, \
-                                                rc, bt.x, bt.ws)
+#define GLL_GRAM(V, N, G)                                                                         \
+    gram_lds_kernel<V, N, G><<<grid, 512, 0, s>>>(X, L.n, L.d, T, KS, kspan, D2, L.ldD, plane, st, \
+                                                   rc, bt.x, bt.ws)
     if (vec) {
-        if (NCH == 4) GLL_GRAM(true, 4); else if (NCH == 2) GLL_GRAM(true, 2); else GLL_GRAM(true, 1);
+        if (NCH == 4) GLL_GRAM(true, 4, GK); else if (NCH == 2) GLL_GRAM(true, 2, GK); else GLL_GRAM(true, 1, GK);
     } else {
-        if (NCH == 4) GLL_GRAM(false, 4); else if (NCH == 2) GLL_GRAM(false, 2); else GLL_GRAM(false, 1);
+        if (NCH == 4) GLL_GRAM(false, 4, GK); else if (NCH == 2) GLL_GRAM(false, 2, GK); else GLL_GRAM(false, 1, GK);
     }
 #undef GLL_GRAM
     prof_end(GLL_K_GRAM, s);
-    return hipGetLastError();
+    return launch_status("knn.hip:launch_gram");
 }
 
 hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float* X,
@@ -520,7 +539,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
 #undef GLL_SEL
 #undef GLL_SEL3
     prof_end(GLL_K_SELECT, s);
-    return hipGetLastError();
+    return launch_status("knn.hip:launch_select");
 }
 
 }  // namespace gll

@@ -310,7 +310,7 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     else if (y_dtype == GLL_DT_I64) row_build_kernel<int64_t><<<grid, 256, 0, s>>>(a, static_cast<const int64_t*>(Y), bt.y);
     else return hipErrorInvalidValue;
     prof_end(GLL_K_FINALIZE, s);
-    return hipGetLastError();
+    return launch_status("rows.hip:launch_finalize");
 }
 
 }  // namespace gll

@@ -20,6 +20,8 @@
 // the CSR).  Only p is published through LDS for the gathers.  Dot products are DPP wave
 // reductions plus one LDS exchange across waves; an iteration has three barriers.
 // cg_lds_kernel: vectors in LDS or global memory, for systems larger than that.
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <unordered_set>
 
@@ -30,14 +32,23 @@ namespace gll {
 GLL_TRACE_UNIT(solve)
 
 static constexpr size_t kLdsLimit = 160 * 1024;
+static constexpr size_t kLdsDyn = kLdsLimit - 1024;   // dynamic share, room for static LDS
 
-// Opt a kernel into the full 160 KiB of dynamic LDS, once per kernel (host-side cost).
+// Opt a kernel into all of the 160 KiB of LDS its static allocation leaves for dynamic use,
+// once per kernel (host-side cost).  The attribute call's status is consumed here: a failure
+// must not linger as the thread's last error and surface at an unrelated launch.
 static void allow_full_lds(const void* fn) {
     static std::mutex mu;
     static std::unordered_set<const void*> done;
     std::lock_guard<std::mutex> lk(mu);
-    if (done.insert(fn).second)
-        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsLimit));
+    if (done.insert(fn).second) {
+        hipFuncAttributes at{};
+        size_t stat = 0;
+        if (hipFuncGetAttributes(&at, fn) == hipSuccess) stat = at.sharedSizeBytes;
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int(kLdsLimit - stat));
+        (void)hipGetLastError();
+    }
 }
 
 // Block-wide sum of two values; every thread gets the totals (fixed order -> deterministic).
@@ -370,12 +381,16 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
     // launches (a full-LDS request would pin one per CU)
     constexpr int64_t kOvfLds = 2048;
     const int64_t eu_bound = int64_t(L.m + L.n) * (L.K - 1);
-    int64_t cap = int64_t(kLdsLimit - lds) / 8;
+    int64_t cap = int64_t(kLdsDyn - lds) / 8;
     if (cap > eu_bound) cap = eu_bound;
     if (cap > kOvfLds) cap = kOvfLds;
     if (cap < 0) cap = 0;
     lds += size_t(cap) * 8;
-    if (S != L.SE) return hipErrorInvalidValue;   // row_build emitted L.SE slots
+    if (S != L.SE) {   // row_build emitted L.SE slots
+        (void)hipGetLastError();
+        if (getenv("GLL_DEBUG")) fprintf(stderr, "gll: run_ell S=%d but ELL width %d\n", S, L.SE);
+        return hipErrorInvalidValue;
+    }
     auto fn = cg_ell_kernel<NT, R, S, TB>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
     fn<<<dim3(L.C, bt.B), NT, lds, s>>>(
@@ -383,7 +398,7 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
         L.at<int32_t>(ws, L.ucnt), L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
         L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, int(cap), st_nonconv, st_iters,
         L.at<int32_t>(ws, L.ell_col), L.at<float>(ws, L.ell_w), bt.ws, bs, bt.u, bt.st);
-    return hipGetLastError();
+    return launch_status("solve.hip:run_ell");
 }
 
 template <typename TB>
@@ -412,7 +427,7 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     if (m <= 4096) GLL_ELL(1024, 4, 4);
 #undef GLL_ELL
     const size_t vec_bytes = size_t(5) * m * sizeof(float);
-    const bool vec_lds = 64 * 4 + vec_bytes <= kLdsLimit;
+    const bool vec_lds = 64 * 4 + vec_bytes <= kLdsDyn;
     const size_t lds = 64 * 4 + (vec_lds ? vec_bytes : 0);
     auto fn = cg_lds_kernel<1024, TB>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
@@ -421,7 +436,7 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
         L.at<int32_t>(ws, L.ucnt), L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
         L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, L.at<float>(ws, L.cgv),
         vec_lds ? 1 : 0, st_nonconv, st_iters, bt.ws, bs, bt.u, bt.st);
-    return hipGetLastError();
+    return launch_status("solve.hip:cg_dispatch");
 }
 
 hipError_t launch_cg_luu(const Layout& L, const Batch& bt, void* ws, const void* b,
@@ -521,7 +536,7 @@ hipError_t launch_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* co
                          const float* val, const float* b, float* x, float atol, int max_iter,
                          int32_t* iters, int32_t* nonconv, float* gvec, hipStream_t s) {
     const size_t vec_bytes = size_t(5) * m * sizeof(float);
-    const bool vec_lds = 64 * 4 + vec_bytes <= kLdsLimit;
+    const bool vec_lds = 64 * 4 + vec_bytes <= kLdsDyn;
     if (!vec_lds && gvec == nullptr) return hipErrorInvalidValue;
     const size_t lds = 64 * 4 + (vec_lds ? vec_bytes : 0);
     auto fn = cg_csr_kernel<256>;
@@ -530,7 +545,7 @@ hipError_t launch_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* co
     fn<<<C, 256, lds, s>>>(m, C, row_ptr, col, val, b, x, atol, max_iter, gvec, vec_lds ? 1 : 0,
                            iters, nonconv);
     prof_end(GLL_K_CG, s);
-    return hipGetLastError();
+    return launch_status("solve.hip:launch_cg_csr");
 }
 
 }  // namespace gll

@@ -42,7 +42,7 @@ extern "C" {
 #define GLL_ST_NWORDS 16
 
 /* gll_problem.flags */
-#define GLL_FLAG_CG_GRID 1   /* solve Luu with the grid-wide CG even when m <= 4096 */
+#define GLL_FLAG_CG_GRID 1   /* solve Luu with the whole-GPU CG even for small m */
 
 typedef struct gll_problem {
     int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */
