@@ -43,6 +43,18 @@ FLUSH_EVERY = 64
 _pending = collections.deque()
 _sinks = {}
 
+# Optional exploding-gradient diagnostic of the adversarial scripts' inline copy
+# (train_and_adversarial.py:177-183): None = off; a float = the matrix-norm threshold.  When on,
+# calls take the Python Function path, whose backward synchronises to test the norm.
+_grad_diag = None
+
+
+def set_grad_diagnostics(threshold=10.0):
+    """Print the reference's 'possible exploding gradient' report when ||grad_X||_F exceeds
+    `threshold` (the inline copy uses 10); None switches the check off (the default)."""
+    global _grad_diag
+    _grad_diag = None if threshold is None else float(threshold)
+
 
 def _sink(dev: torch.device):
     s = _sinks.get(dev.index)
@@ -177,7 +189,7 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
     @classmethod
     def apply(cls, X, label_matrix, tau=0, epsilon="auto", k=DEFAULT_K):
         ext = _ext()
-        if ext is None:
+        if ext is None or _grad_diag is not None:
             return super().apply(X, label_matrix, tau, epsilon, k)
         if _pending:
             _poll_status()
@@ -245,6 +257,20 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
                                                        ctx.ws.data_ptr(), g.data_ptr(), gdt,
                                                        gradX.data_ptr(), _stream(dev)),
                        "gll_backward")
+        if _grad_diag is not None:
+            out_norm = torch.linalg.vector_norm(gradX).item()
+            if out_norm > _grad_diag:     # train_and_adversarial.py:177-183
+                m = prob.n - prob.base
+                wadj = ctx.ws.new_empty(0)
+                view = _lib.View()
+                _lib.check(_lib.lib().gll_workspace_view(ct.byref(prob), ctx.ws.data_ptr(),
+                                                         ct.byref(view)), "gll_workspace_view")
+                off = view.wadj - ctx.ws.data_ptr()
+                wadj = ctx.ws[off: off + 4 * m * prob.C].view(torch.float32)
+                print("possible exploding gradient")
+                print("grad norm: ", torch.linalg.vector_norm(g.double()).item())
+                print("w norm: ", torch.linalg.vector_norm(wadj.double()).item())
+                print("out norm: ", out_norm)
         if gradX.device != X.device or gradX.dtype != X.dtype:
             gradX = gradX.to(device=X.device, dtype=X.dtype)
         return gradX, None, None, None, None

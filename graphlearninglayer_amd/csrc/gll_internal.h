@@ -42,7 +42,7 @@ inline int ell_slots(int m) {
 #ifdef GLL_TRACE
 #define GLL_TRACE_UNIT(name)                                                                 \
     static __device__ unsigned long long g_trace[64];                                       \
-    static __device__ unsigned long long g_wg[3 * 4096]; /* kernel 0: entry, exit, cu id */ \
+    static __device__ unsigned long long g_wg[2 * 3 * 4096]; /* kernels 0-1: entry, exit, cu */ \
     void trace_read_##name(unsigned long long* out) {                                       \
         (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), sizeof(g_trace));               \
     }                                                                                        \
@@ -61,9 +61,9 @@ inline int ell_slots(int m) {
                 const unsigned long long t = __builtin_amdgcn_s_memrealtime();               \
                 atomicMin(&g_trace[32 + 2 * k], t);                                          \
                 atomicMax(&g_trace[24 + k], t);                                              \
-                if (k == 0 && blockIdx.x < 4096) {                                           \
-                    g_wg[blockIdx.x] = t;                                                    \
-                    g_wg[2 * 4096 + blockIdx.x] = __smid();                                  \
+                if (k < 2 && blockIdx.x < 4096 && blockIdx.y == 0) {                         \
+                    g_wg[k * 3 * 4096 + blockIdx.x] = t;                                     \
+                    g_wg[k * 3 * 4096 + 2 * 4096 + blockIdx.x] = __smid();                   \
                 }                                                                            \
             }                                                                                \
         }                                                                                    \
@@ -71,7 +71,8 @@ inline int ell_slots(int m) {
             if (threadIdx.x == 0) {                                                          \
                 const unsigned long long t = __builtin_amdgcn_s_memrealtime();               \
                 atomicMax(&g_trace[33 + 2 * k], t);                                          \
-                if (k == 0 && blockIdx.x < 4096) g_wg[4096 + blockIdx.x] = t;                \
+                if (k < 2 && blockIdx.x < 4096 && blockIdx.y == 0)                           \
+                    g_wg[k * 3 * 4096 + 4096 + blockIdx.x] = t;                              \
             }                                                                                \
         }                                                                                    \
     };

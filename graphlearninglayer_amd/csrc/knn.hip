@@ -353,6 +353,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     int32_t* __restrict__ status, int32_t* __restrict__ status_pub, size_t xs, size_t wss,
     size_t sts) {
     GLL_TRACE_SCOPE(1);
+    GLL_TRACE_PT(20);
     D2 = gshift(D2, wss);
     X = gshift(X, xs);
     knn_idx = gshift(knn_idx, wss);
@@ -384,38 +385,51 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
             ci = merge_exact<KC>(full, kc);
         }
     }
-    // 3) exact squared distances, 8 candidates per pass (8 lanes each, across d)
+    // 3) exact squared distances: 8 lanes per candidate across d, two groups of 8 candidates
+    //    per sweep with every load of the sweep in flight at once (x_i loaded once for both)
     const int grp = lane >> 3, sub = lane & 7;
     const float* xi = X + size_t(i) * d;
     float ce = __builtin_inff();
-    for (int p0 = 0; p0 < kc; p0 += 8) {
-        const int j = __shfl(ci, p0 + grp < kc ? p0 + grp : 0);
-        const bool live = p0 + grp < kc && j >= 0;
-        const float* xj = X + size_t(live ? j : i) * d;
-        float part = 0.f;
-        for (int kb = 0; kb < d; kb += 512) {   // 16 steps of 32 features: all loads in flight
-            f32x4 va[16], vb[16];
+    for (int p0 = 0; p0 < kc; p0 += 16) {
+        const int ja = __shfl(ci, p0 + grp < kc ? p0 + grp : 0);
+        const int jb = __shfl(ci, p0 + 8 + grp < kc ? p0 + 8 + grp : 0);
+        const bool la = p0 + grp < kc && ja >= 0;
+        const bool lb = p0 + 8 + grp < kc && jb >= 0;
+        const float* xja = X + size_t(la ? ja : i) * d;
+        const float* xjb = X + size_t(lb ? jb : i) * d;
+        float pa = 0.f, pb = 0.f;
+        for (int kb = 0; kb < d; kb += 512) {   // 16 steps of 32 features
+            f32x4 va[16], wa[16], wb[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) {   // straight-line: every load issued before use
                 const int k = kb + 32 * u + 4 * sub;
                 va[u] = load4_raw<VEC>(xi, k, d);
-                vb[u] = load4_raw<VEC>(xj, k, d);
+                wa[u] = load4_raw<VEC>(xja, k, d);
+                wb[u] = load4_raw<VEC>(xjb, k, d);
             }
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
+            for (int u = 0; u < 16; ++u) {   // same order per pair from either end: symmetric
                 const int k = kb + 32 * u + 4 * sub;
-                const f32x4 df = mask4<VEC>(va[u] - vb[u], k, d);
-                part += df.x * df.x;
-                part += df.y * df.y;
-                part += df.z * df.z;
-                part += df.w * df.w;
+                const f32x4 da = mask4<VEC>(va[u] - wa[u], k, d);
+                const f32x4 db = mask4<VEC>(va[u] - wb[u], k, d);
+                pa += da.x * da.x;
+                pa += da.y * da.y;
+                pa += da.z * da.z;
+                pa += da.w * da.w;
+                pb += db.x * db.x;
+                pb += db.y * db.y;
+                pb += db.z * db.z;
+                pb += db.w * db.w;
             }
         }
-        part = group8_sum(part);
+        pa = group8_sum(pa);
+        pb = group8_sum(pb);
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            const float v = readlane_f(part, 8 * g);
-            if (lane == p0 + g) ce = v;
+            const float vA = readlane_f(pa, 8 * g);
+            const float vB = readlane_f(pb, 8 * g);
+            if (lane == p0 + g) ce = vA;
+            if (lane == p0 + 8 + g) ce = vB;
         }
     }
     GLL_TRACE_PT(18);

@@ -34,15 +34,22 @@ for _ in range(10):
     lib.gll_forward(ct.byref(prob), ct.c_void_p(X.data_ptr()), ct.c_void_p(Y.data_ptr()), 0,
                     ct.c_void_p(ws.data_ptr()), ct.c_void_p(U.data_ptr()), s)
 torch.cuda.synchronize()
-buf = (ct.c_ulonglong * (3 * 4096))()
+KERNEL = int(os.environ.get("PROBE_KERNEL", "0"))   # 0 gram, 1 select
+if KERNEL == 1:
+    nwg = (n + 3) // 4
+buf = (ct.c_ulonglong * (2 * 3 * 4096))()
 lib.gll_trace_read_wg(0, buf)
-a = np.array(buf[:], dtype=np.int64).reshape(3, 4096)[:, :nwg]
+a = np.array(buf[:], dtype=np.uint64).astype(np.int64).reshape(2, 3, 4096)[KERNEL][:, :nwg]
 ent, ext, cu = a[0], a[1], a[2]
 t0 = ent.min()
 ent = (ent - t0) / 100.0
 ext = (ext - t0) / 100.0
-print(f"workgroups {nwg}: entry spread {ent.max():.2f} us, last exit {ext.max():.2f} us, "
+print(f"kernel {KERNEL} workgroups {nwg}: entry spread {ent.max():.2f} us, last exit {ext.max():.2f} us, "
       f"duration mean {np.mean(ext - ent):.2f} min {np.min(ext - ent):.2f} max {np.max(ext - ent):.2f}")
+dur = ext - ent
+print("duration percentiles (us) 10/50/90/99/max:",
+      " ".join(f"{np.percentile(dur, q):.2f}" for q in (10, 50, 90, 99, 100)))
+print("slowest 8 workgroups:", " ".join(f"{int(b)}:{dur[b]:.1f}" for b in np.argsort(dur)[-8:]))
 for t in np.arange(0, ext.max() + 1, 1.0):
     print(f"  t={t:5.1f} resident {int(np.sum((ent <= t) & (ext > t)))}")
 xcc = cu >> 6

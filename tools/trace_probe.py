@@ -88,9 +88,10 @@ def timeline(tr, label):
         print("gram block 0: " + ", ".join(f"{nm} +{TICK_US * (g[q] - g[10]):.2f}" for q, nm in
                                           [(15, "chunk0 in LDS"), (11, "mfma done"), (12, "loop exit"),
                                            (13, "tile staged"), (14, "stored")] if g[q]))
-    if g[16]:
-        print("select wave 0: " + ", ".join(f"{nm} +{TICK_US * (g[q] - g[16]):.2f}" for q, nm in
-                                           [(17, "merged"), (18, "refined"), (19, "ranked+written")] if g[q]))
+    if g[16] and g[20]:
+        print("select wave 0: " + ", ".join(f"{nm} +{TICK_US * (g[q] - g[20]):.2f}" for q, nm in
+                                           [(16, "scanned"), (17, "merged"), (18, "refined"),
+                                            (19, "ranked+written")] if g[q]))
     pts = tr[2][:10].astype(np.int64)
     if pts[0]:
         print("cg block 0: " + ", ".join(f"{CG_PTS[i]} +{TICK_US * (pts[i] - pts[0]):.2f}"
