@@ -95,6 +95,9 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
         for (int q = g; q < n; q += gridDim.x * 512) rev_cnt[q] = 0;
     }
     GLL_TRACE_PT(10);
+#ifdef GLL_TRACE
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_trace[21] = __builtin_amdgcn_s_memtime();
+#endif
     const int k_lo = ks * kspan;
     const int k_hi = min(d, k_lo + kspan);
     const int nsup = kspan / (GK * NCH);
@@ -224,6 +227,173 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
         }
     }
     GLL_TRACE_PT(14);
+#ifdef GLL_TRACE
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_trace[22] = __builtin_amdgcn_s_memtime();
+#endif
+}
+
+// --------------------------------------------------------------------------------------
+// K1a': wide symmetric Gram tile for large problems (many tiles): 128 x 128 per workgroup, 4
+// waves each owning a 64 x 64 sub-tile as 2 x 2 independent 32 x 32 MFMA accumulators (one
+// A fragment feeds two MFMAs, four chains keep the MFMA pipe full from one wave per SIMD),
+// 32-deep chunks through a register ring of NCH chunks into double-buffered LDS.
+// --------------------------------------------------------------------------------------
+constexpr int kWK = 32;           // k per chunk
+constexpr int kWL = kWK + 4;      // padded LDS row (floats)
+
+template <bool VEC, int NCH>
+__global__ __launch_bounds__(256) void gram_wide_kernel(const float* __restrict__ X, int n, int d,
+                                                        int T, float* __restrict__ D2, int ld,
+                                                        int32_t* __restrict__ status,
+                                                        int32_t* __restrict__ rev_cnt,
+                                                        size_t xs, size_t wss) {
+    GLL_TRACE_SCOPE(2);
+    X = gshift(X, xs);
+    D2 = gshift(D2, wss);
+    status = gshift(status, wss);
+    rev_cnt = gshift(rev_cnt, wss);
+    // stage[buf][A|B][128][kWL]; the epilogue reuses it as tile[128][129]
+    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * 128 * kWL];
+    __shared__ float s_sq[2][128];
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;   // 64-row / 64-column half of the tile
+    const int r = lane & 31, h = lane >> 5;
+    int bi = 0, rem = blockIdx.x;
+    while (rem >= T - bi) {
+        rem -= T - bi;
+        ++bi;
+    }
+    const int bj = bi + rem;
+    {   // per-call reset of the counters the select kernel accumulates into
+        const int g = blockIdx.x * 256 + tid;
+        if (g < GLL_ST_NWORDS) status[g] = 0;
+        for (int q = g; q < n; q += gridDim.x * 256) rev_cnt[q] = 0;
+    }
+    // loader: thread t moves float4 column 4 (t & 7) of rows (t >> 3) + 32 s, s < 4, of A and B
+    const int lrow = tid >> 3, lcol = 4 * (tid & 7);
+    const float* ga[4];
+    const float* gb[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+        ga[s4] = X + size_t(min(bi * 128 + lrow + 32 * s4, n - 1)) * d;
+        gb[s4] = X + size_t(min(bj * 128 + lrow + 32 * s4, n - 1)) * d;
+    }
+    const int nchunk = (d + kWK - 1) / kWK;
+    const int nsup = (nchunk + NCH - 1) / NCH;
+    f32x4 ring[NCH][8];
+    auto gload = [&](int chunk, f32x4 (&v)[8]) {   // raw: masked when stored to LDS
+        const int k = chunk * kWK + lcol;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            v[s4] = load4_raw<VEC>(ga[s4], k, d);
+            v[4 + s4] = load4_raw<VEC>(gb[s4], k, d);
+        }
+    };
+    auto lstore = [&](int chunk, int buf, const f32x4 (&v)[8]) {
+        const int k = chunk * kWK + lcol;
+        float* A = smem + (buf * 2 + 0) * 128 * kWL;
+        float* B = smem + (buf * 2 + 1) * 128 * kWL;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            *reinterpret_cast<f32x4*>(A + (lrow + 32 * s4) * kWL + lcol) = mask4<VEC>(v[s4], k, d);
+            *reinterpret_cast<f32x4*>(B + (lrow + 32 * s4) * kWL + lcol) = mask4<VEC>(v[4 + s4], k, d);
+        }
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.f;
+    float sa[2] = {0.f, 0.f}, sb[2] = {0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) gload(min(c, nchunk - 1), ring[c]);
+    for (int sc = 0; sc < nsup; ++sc) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int chunk = sc * NCH + c;
+            if (chunk >= nchunk) break;   // uniform
+            const int buf = chunk & 1;
+            lstore(chunk, buf, ring[c]);
+            gload(min(chunk + NCH, nchunk - 1), ring[c]);   // unconditional: static counts
+            __syncthreads();
+            const float* A = smem + (buf * 2 + 0) * 128 * kWL;
+            const float* B = smem + (buf * 2 + 1) * 128 * kWL;
+            f32x4 a[2][4], b[2][4];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    a[i][u] = *reinterpret_cast<const f32x4*>(A + (64 * wr + 32 * i + r) * kWL + 4 * h + 8 * u);
+                    b[i][u] = *reinterpret_cast<const f32x4*>(B + (64 * wc + 32 * i + r) * kWL + 4 * h + 8 * u);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][u][t], b[j][u][t],
+                                                                           acc[i][j], 0, 0, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    sa[i] += a[i][u].x * a[i][u].x + a[i][u].y * a[i][u].y +
+                             a[i][u].z * a[i][u].z + a[i][u].w * a[i][u].w;
+                    sb[i] += b[i][u].x * b[i][u].x + b[i][u].y * b[i][u].y +
+                             b[i][u].z * b[i][u].z + b[i][u].w * b[i][u].w;
+                }
+            }
+        }
+    }
+    __syncthreads();   // (one barrier per chunk suffices: buffer `buf` is rewritten only after
+                       //  every wave has passed the next chunk's barrier)
+    // row norms: the two k-quarters of a lane pair (xor 32), A rows from wc == 0 waves, B rows
+    // (columns) from wr == 0 waves
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        sa[i] += __shfl_xor(sa[i], 32);
+        sb[i] += __shfl_xor(sb[i], 32);
+        if (h == 0 && wc == 0) s_sq[0][64 * wr + 32 * i + r] = sa[i];
+        if (h == 0 && wr == 0) s_sq[1][64 * wc + 32 * i + r] = sb[i];
+    }
+    __syncthreads();
+    float* tile = smem;   // [128][129]
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int tc = 64 * wc + 32 * j + r;
+            const float sqc = s_sq[1][tc];
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int tr = 64 * wr + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
+                tile[tr * 129 + tc] = s_sq[0][tr] + sqc - 2.f * acc[i][j][g];
+            }
+        }
+    }
+    __syncthreads();
+    const int cr = tid >> 5, cc = (tid & 31) * 4;
+    for (int rr = cr; rr < 128; rr += 8) {
+        const int i = bi * 128 + rr;
+        if (i < n) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (bj * 128 + cc + t < n) D2[size_t(i) * ld + bj * 128 + cc + t] = tile[rr * 129 + cc + t];
+        }
+        const int jr = bj * 128 + rr;
+        if (bi != bj && jr < n) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (bi * 128 + cc + t < n) D2[size_t(jr) * ld + bi * 128 + cc + t] = tile[(cc + t) * 129 + rr];
+        }
+    }
 }
 
 // --------------------------------------------------------------------------------------
@@ -385,51 +555,40 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
             ci = merge_exact<KC>(full, kc);
         }
     }
-    // 3) exact squared distances: 8 lanes per candidate across d, two groups of 8 candidates
-    //    per sweep with every load of the sweep in flight at once (x_i loaded once for both)
+    // 3) exact squared distances, 8 candidates per pass (8 lanes each, across d).  (Two
+    //    groups per sweep -- every load in flight at once -- saved ~0.2 us at NS but took 191
+    //    VGPRs; with B graphs or large n the lost occupancy cost 20-45%: kept one group.)
     const int grp = lane >> 3, sub = lane & 7;
     const float* xi = X + size_t(i) * d;
     float ce = __builtin_inff();
-    for (int p0 = 0; p0 < kc; p0 += 16) {
-        const int ja = __shfl(ci, p0 + grp < kc ? p0 + grp : 0);
-        const int jb = __shfl(ci, p0 + 8 + grp < kc ? p0 + 8 + grp : 0);
-        const bool la = p0 + grp < kc && ja >= 0;
-        const bool lb = p0 + 8 + grp < kc && jb >= 0;
-        const float* xja = X + size_t(la ? ja : i) * d;
-        const float* xjb = X + size_t(lb ? jb : i) * d;
-        float pa = 0.f, pb = 0.f;
-        for (int kb = 0; kb < d; kb += 512) {   // 16 steps of 32 features
-            f32x4 va[16], wa[16], wb[16];
+    for (int p0 = 0; p0 < kc; p0 += 8) {
+        const int j = __shfl(ci, p0 + grp < kc ? p0 + grp : 0);
+        const bool live = p0 + grp < kc && j >= 0;
+        const float* xj = X + size_t(live ? j : i) * d;
+        float part = 0.f;
+        for (int kb = 0; kb < d; kb += 512) {   // 16 steps of 32 features: all loads in flight
+            f32x4 va[16], vb[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) {   // straight-line: every load issued before use
                 const int k = kb + 32 * u + 4 * sub;
                 va[u] = load4_raw<VEC>(xi, k, d);
-                wa[u] = load4_raw<VEC>(xja, k, d);
-                wb[u] = load4_raw<VEC>(xjb, k, d);
+                vb[u] = load4_raw<VEC>(xj, k, d);
             }
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {   // same order per pair from either end: symmetric
+            for (int u = 0; u < 16; ++u) {   // same order from either end: symmetric in (i, j)
                 const int k = kb + 32 * u + 4 * sub;
-                const f32x4 da = mask4<VEC>(va[u] - wa[u], k, d);
-                const f32x4 db = mask4<VEC>(va[u] - wb[u], k, d);
-                pa += da.x * da.x;
-                pa += da.y * da.y;
-                pa += da.z * da.z;
-                pa += da.w * da.w;
-                pb += db.x * db.x;
-                pb += db.y * db.y;
-                pb += db.z * db.z;
-                pb += db.w * db.w;
+                const f32x4 df = mask4<VEC>(va[u] - vb[u], k, d);
+                part += df.x * df.x;
+                part += df.y * df.y;
+                part += df.z * df.z;
+                part += df.w * df.w;
             }
         }
-        pa = group8_sum(pa);
-        pb = group8_sum(pb);
+        part = group8_sum(part);
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            const float vA = readlane_f(pa, 8 * g);
-            const float vB = readlane_f(pb, 8 * g);
-            if (lane == p0 + g) ce = vA;
-            if (lane == p0 + 8 + g) ce = vB;
+            const float v = readlane_f(part, 8 * g);
+            if (lane == p0 + g) ce = v;
         }
     }
     GLL_TRACE_PT(18);
@@ -487,8 +646,32 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     }
 }
 
+// Wide 128-tiles when there are enough of them to fill the chip twice over (large graphs and
+// batches); the 64-tile kernel otherwise (a single NS graph has only 36 wide tiles).
+static bool use_wide_gram(const Layout& L, const Batch& bt) {
+    if (L.KS != 1 || (L.flags & GLL_FLAG_GRAM_NARROW)) return false;
+    const int64_t T = (L.n + 127) / 128;
+    return int64_t(bt.B) * T * (T + 1) / 2 >= 512;
+}
+
 hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
                        hipStream_t s) {
+    if (use_wide_gram(L, bt)) {
+        const int T = (L.n + 127) / 128;
+        const dim3 grid(T * (T + 1) / 2, bt.B);
+        float* D2 = L.at<float>(ws, L.D2);
+        int32_t* st = L.at<int32_t>(ws, L.status);
+        int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
+        const int nchunk = (L.d + kWK - 1) / kWK;
+        prof_begin(GLL_K_GRAM, s);
+#define GLL_WIDE(V, N) \
+    gram_wide_kernel<V, N><<<grid, 256, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws)
+        if (vec) { if (nchunk >= 2) GLL_WIDE(true, 2); else GLL_WIDE(true, 1); }
+        else { if (nchunk >= 2) GLL_WIDE(false, 2); else GLL_WIDE(false, 1); }
+#undef GLL_WIDE
+        prof_end(GLL_K_GRAM, s);
+        return launch_status("knn.hip:launch_gram(wide)");
+    }
     const int T = (L.n + 63) / 64;
     const int tiles = T * (T + 1) / 2;
     const int KS = L.KS;

@@ -42,7 +42,8 @@ extern "C" {
 #define GLL_ST_NWORDS 16
 
 /* gll_problem.flags */
-#define GLL_FLAG_CG_GRID 1   /* solve Luu with the whole-GPU CG even for small m */
+#define GLL_FLAG_CG_GRID 1      /* solve Luu with the whole-GPU CG even for small m */
+#define GLL_FLAG_GRAM_NARROW 2  /* Gram on 64-tiles even where 128-tiles apply (diagnostic) */
 
 typedef struct gll_problem {
     int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */

@@ -1,7 +1,7 @@
 """Per-kernel time under gll_problem.flags variants (diagnostic A/B, GPU box).
 
-FLAGS env: comma list of gll_problem.flags values to compare (default "0,1": per-column vs
-whole-GPU CG)."""
+FLAGS env: comma list of gll_problem.flags values to compare (default "0,2": wide 128-tile
+Gram vs 64-tile Gram; "0,1": per-column vs whole-GPU CG)."""
 import ctypes as ct
 import os
 import sys
@@ -15,7 +15,7 @@ from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth  #
 
 lib = _lib.lib()
 names = [_lib.kernel_name(q) for q in range(_lib.K_COUNT)]
-flags_list = [int(f) for f in os.environ.get("FLAGS", "0,1").split(",")]
+flags_list = [int(f) for f in os.environ.get("FLAGS", "0,2").split(",")]
 for cfg, eps, B in [("ns", 1.0, 1), ("ns", 1.0, 64), ("stress", "auto", 1)]:
     c = CONFIGS[cfg]
     n = c["base"] + c["batch"]

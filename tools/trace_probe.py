@@ -88,6 +88,9 @@ def timeline(tr, label):
         print("gram block 0: " + ", ".join(f"{nm} +{TICK_US * (g[q] - g[10]):.2f}" for q, nm in
                                           [(15, "chunk0 in LDS"), (11, "mfma done"), (12, "loop exit"),
                                            (13, "tile staged"), (14, "stored")] if g[q]))
+    if g[21] and g[22] and g[14] > g[10]:
+        mhz = (g[22] - g[21]) / ((g[14] - g[10]) / 100.0)
+        print(f"gram block 0: shader clock {mhz:.0f} MHz (s_memtime / s_memrealtime)")
     if g[16] and g[20]:
         print("select wave 0: " + ", ".join(f"{nm} +{TICK_US * (g[q] - g[20]):.2f}" for q, nm in
                                            [(16, "scanned"), (17, "merged"), (18, "refined"),
