@@ -44,17 +44,20 @@ GLL_TRACE_UNIT(knn)
 // ds_read_b128).  128-deep chunks halve the barriers per tile (one LDS turnaround each).
 constexpr int kGK = 64;
 
-// 16 MFMAs over 32 k: lane (r, h) holds A[r][8u + 4h + t], B[c=r][8u + 4h + t]
+// 16 MFMAs over 32 k: lane (r, h) holds A[r][8u + 4h + t], B[c=r][8u + 4h + t].  Two
+// independent accumulator chains (alternate u) -- with 2 waves per SIMD that keeps four
+// chains in flight per SIMD, what the fp32 MFMA needs to issue every 64 cycles.
 __device__ __forceinline__ void gram_chunk_mfma(const f32x4 (&a)[4], const f32x4 (&b)[4],
-                                                f32x16& acc, float& sa, float& sb) {
+                                                f32x16 (&acc)[2], float& sa, float& sb) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         sa += a[u].x * a[u].x + a[u].y * a[u].y + a[u].z * a[u].z + a[u].w * a[u].w;
         sb += b[u].x * b[u].x + b[u].y * b[u].y + b[u].z * b[u].z + b[u].w * b[u].w;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].x, b[u].x, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].y, b[u].y, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].z, b[u].z, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].w, b[u].w, acc, 0, 0, 0);
+        f32x16& c = acc[u & 1];
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].x, b[u].x, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].y, b[u].y, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].z, b[u].z, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].w, b[u].w, c, 0, 0, 0);
     }
 }
 
@@ -132,9 +135,9 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
             *reinterpret_cast<f32x4*>(B + (lrow + 32) * kGL + col) = mask4<VEC>(v[4 * cs + 3], k, k_hi);
         }
     };
-    f32x16 acc;
+    f32x16 acc2[2];
 #pragma unroll
-    for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+    for (int g = 0; g < 16; ++g) acc2[0][g] = acc2[1][g] = 0.f;
     float sa = 0.f, sb = 0.f;
     const int arow = (qd >> 1) * 32 + r, brow = (qd & 1) * 32 + r;
 #pragma unroll
@@ -163,7 +166,7 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
                     a[u] = *reinterpret_cast<const f32x4*>(A + 8 * u);
                     b[u] = *reinterpret_cast<const f32x4*>(B + 8 * u);
                 }
-                gram_chunk_mfma(a, b, acc, sa, sb);
+                gram_chunk_mfma(a, b, acc2, sa, sb);
             }
         }
     };
@@ -175,6 +178,7 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
     }
     __syncthreads();
     GLL_TRACE_PT(12);
+    f32x16 acc = acc2[0] + acc2[1];
     // combine the k-halves in a fixed order (half 0 + half 1) through LDS
     float* part = smem;                    // [4 quadrants][16][64]
     float* nrm = smem + 4 * 16 * 64;       // [2][4][64]
@@ -681,7 +685,7 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
     constexpr int GK = kGK;
     const int dsl = (L.d + KS - 1) / KS;
     int kspan = (dsl + GK - 1) / GK * GK;
-    const int NCH = kspan >= 4 * GK ? 4 : (kspan >= 2 * GK ? 2 : 1);
+    const int NCH = kspan >= 2 * GK ? 2 : 1;   // (4 spills beside two accumulator chains)
     kspan = (kspan + NCH * GK - 1) / (NCH * GK) * (NCH * GK);
     float* D2 = L.at<float>(ws, L.D2);
     const size_t plane = size_t(L.n) * L.ldD;
@@ -693,9 +697,9 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
     gram_lds_kernel<V, N, G><<<grid, 512, 0, s>>>(X, L.n, L.d, T, KS, kspan, D2, L.ldD, plane, st, \
                                                    rc, bt.x, bt.ws)
     if (vec) {
-        if (NCH == 4) GLL_GRAM(true, 4, GK); else if (NCH == 2) GLL_GRAM(true, 2, GK); else GLL_GRAM(true, 1, GK);
+        if (NCH == 2) GLL_GRAM(true, 2, GK); else GLL_GRAM(true, 1, GK);
     } else {
-        if (NCH == 4) GLL_GRAM(false, 4, GK); else if (NCH == 2) GLL_GRAM(false, 2, GK); else GLL_GRAM(false, 1, GK);
+        if (NCH == 2) GLL_GRAM(false, 2, GK); else GLL_GRAM(false, 1, GK);
     }
 #undef GLL_GRAM
     prof_end(GLL_K_GRAM, s);
