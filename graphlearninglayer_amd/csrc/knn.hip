@@ -237,6 +237,160 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
 }
 
 // --------------------------------------------------------------------------------------
+// K1a'': 48 x 48 tiles for small problems, where 64-tiles leave CUs idle (n = 1000: 136 64-tiles
+// vs 231 48-tiles for 256 CUs).  v_mfma_f32_16x16x4f32 (A[l&15][k=l>>4], B[k=l>>4][l&15];
+// C col = l&15, row = 4(l>>4) + reg).  12 waves = 4 k-quarters of each 64-deep chunk x 3
+// row blocks; a wave owns the 3 blocks of its row (3 independent accumulators).  Lane group
+// g = l >> 4 takes k = 16 kq + 4 g + s at step s, so one ds_read_b128 feeds 4 MFMA steps.
+// --------------------------------------------------------------------------------------
+constexpr int k48L = kGK + 4;   // padded LDS row (floats)
+
+template <bool VEC, int NCH>
+__global__ __launch_bounds__(768) void gram48_kernel(const float* __restrict__ X, int n, int d,
+                                                     int T, float* __restrict__ D2, int ld,
+                                                     int32_t* __restrict__ status,
+                                                     int32_t* __restrict__ rev_cnt,
+                                                     size_t xs, size_t wss) {
+    GLL_TRACE_SCOPE(3);
+    X = gshift(X, xs);
+    D2 = gshift(D2, wss);
+    status = gshift(status, wss);
+    rev_cnt = gshift(rev_cnt, wss);
+    // stage[buf][A|B][48][k48L]; the epilogue reuses it: partials [4][3][3][4][64], norms
+    // 2 x [4][3][64], tile [48][49] -- sized for the larger of the two
+    constexpr int kStage = 2 * 2 * 48 * k48L;
+    constexpr int kEpi = 4 * 3 * 3 * 256 + 2 * 4 * 3 * 64 + 48 * 49;
+    __shared__ __attribute__((aligned(16))) float smem[kStage > kEpi ? kStage : kEpi];
+    __shared__ float s_sq[2][48];
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int wave = tid >> 6;
+    const int kq = wave / 3, rb = wave % 3;
+    const int lr = lane & 15, lg = lane >> 4;
+    int bi = 0, rem = blockIdx.x;
+    while (rem >= T - bi) {
+        rem -= T - bi;
+        ++bi;
+    }
+    const int bj = bi + rem;
+    {   // per-call reset of the counters the select kernel accumulates into
+        const int g = blockIdx.x * 768 + tid;
+        if (g < GLL_ST_NWORDS) status[g] = 0;
+        for (int q = g; q < n; q += gridDim.x * 768) rev_cnt[q] = 0;
+    }
+    // loader: thread t moves float4 column 4 (t & 15) of row t >> 4 (< 48) of A and of B
+    const int lrow = tid >> 4, lcol = 4 * (tid & 15);
+    const float* ga = X + size_t(min(bi * 48 + lrow, n - 1)) * d;
+    const float* gb = X + size_t(min(bj * 48 + lrow, n - 1)) * d;
+    const int nchunk = (d + kGK - 1) / kGK;
+    const int nsup = (nchunk + NCH - 1) / NCH;
+    f32x4 ring[NCH][2];
+    auto gload = [&](int chunk, f32x4 (&v)[2]) {
+        const int k = chunk * kGK + lcol;
+        v[0] = load4_raw<VEC>(ga, k, d);
+        v[1] = load4_raw<VEC>(gb, k, d);
+    };
+    auto lstore = [&](int chunk, int buf, const f32x4 (&v)[2]) {
+        const int k = chunk * kGK + lcol;
+        float* A = smem + (buf * 2 + 0) * 48 * k48L;
+        float* B = smem + (buf * 2 + 1) * 48 * k48L;
+        *reinterpret_cast<f32x4*>(A + lrow * k48L + lcol) = mask4<VEC>(v[0], k, d);
+        *reinterpret_cast<f32x4*>(B + lrow * k48L + lcol) = mask4<VEC>(v[1], k, d);
+    };
+    f32x4 acc[3];
+#pragma unroll
+    for (int cb = 0; cb < 3; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float sa = 0.f, sb[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) gload(min(c, nchunk - 1), ring[c]);
+    for (int sc = 0; sc < nsup; ++sc) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int chunk = sc * NCH + c;
+            if (chunk >= nchunk) break;   // uniform
+            const int buf = chunk & 1;
+            lstore(chunk, buf, ring[c]);
+            gload(min(chunk + NCH, nchunk - 1), ring[c]);   // unconditional: static counts
+            __syncthreads();
+            const int ko = 16 * kq + 4 * lg;
+            const float* A = smem + (buf * 2 + 0) * 48 * k48L;
+            const float* B = smem + (buf * 2 + 1) * 48 * k48L;
+            const f32x4 a = *reinterpret_cast<const f32x4*>(A + (16 * rb + lr) * k48L + ko);
+            f32x4 b[3];
+#pragma unroll
+            for (int cb = 0; cb < 3; ++cb)
+                b[cb] = *reinterpret_cast<const f32x4*>(B + (16 * cb + lr) * k48L + ko);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+#pragma unroll
+                for (int cb = 0; cb < 3; ++cb)
+                    acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[cb][t], acc[cb], 0, 0, 0);
+            }
+            sa += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+#pragma unroll
+            for (int cb = 0; cb < 3; ++cb)
+                sb[cb] += b[cb].x * b[cb].x + b[cb].y * b[cb].y + b[cb].z * b[cb].z + b[cb].w * b[cb].w;
+        }
+    }
+    __syncthreads();
+    // combine the k-quarters in a fixed order through LDS
+    float* part = smem;                     // [kq][rb][cb][4][64]
+    float* nA = smem + 4 * 3 * 3 * 256;     // [kq][rb][64]
+    float* nB = nA + 4 * 3 * 64;            // [kq][cb][64]   (rb == 0 waves)
+#pragma unroll
+    for (int cb = 0; cb < 3; ++cb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) part[(((kq * 3 + rb) * 3 + cb) * 4 + g) * 64 + lane] = acc[cb][g];
+    nA[(kq * 3 + rb) * 64 + lane] = sa;
+    if (rb == 0) {
+#pragma unroll
+        for (int cb = 0; cb < 3; ++cb) nB[(kq * 3 + cb) * 64 + lane] = sb[cb];
+    }
+    __syncthreads();
+    if (tid < 96) {   // row norms: 48 A rows, 48 B rows; sum over k-quarters and lane groups
+        const int which = tid / 48, row = tid % 48, blk = row >> 4, r16 = row & 15;
+        const float* src = which == 0 ? nA : nB;
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) s += src[(q * 3 + blk) * 64 + g * 16 + r16];
+        s_sq[which][row] = s;
+    }
+    __syncthreads();
+    float* tile = nB + 4 * 3 * 64;          // [48][49]
+    if (kq == 0) {
+#pragma unroll
+        for (int cb = 0; cb < 3; ++cb) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float v = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v += part[(((q * 3 + rb) * 3 + cb) * 4 + g) * 64 + lane];
+                const int tr = 16 * rb + 4 * lg + g, tc = 16 * cb + lr;
+                tile[tr * 49 + tc] = s_sq[0][tr] + s_sq[1][tc] - 2.f * v;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < 48 * 12) {   // 48 rows x 12 groups of 4 columns, both orientations
+        const int rr = tid / 12, cc = (tid % 12) * 4;
+        const int i = bi * 48 + rr;
+        if (i < n) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (bj * 48 + cc + t < n) D2[size_t(i) * ld + bj * 48 + cc + t] = tile[rr * 49 + cc + t];
+        }
+        const int jr = bj * 48 + rr;
+        if (bi != bj && jr < n) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (bi * 48 + cc + t < n) D2[size_t(jr) * ld + bi * 48 + cc + t] = tile[(cc + t) * 49 + rr];
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------------
 // K1a': wide symmetric Gram tile for large problems (many tiles): 128 x 128 per workgroup, 4
 // waves each owning a 64 x 64 sub-tile as 2 x 2 independent 32 x 32 MFMA accumulators (one
 // A fragment feeds two MFMAs, four chains keep the MFMA pipe full from one wave per SIMD),
@@ -658,8 +812,31 @@ static bool use_wide_gram(const Layout& L, const Batch& bt) {
     return int64_t(bt.B) * T * (T + 1) / 2 >= 512;
 }
 
+// 48-tiles when 64-tiles would leave a quarter of the CUs idle and 48-tiles fit in one round.
+static bool use_gram48(const Layout& L, const Batch& bt) {
+    if (L.KS != 1 || (L.flags & GLL_FLAG_GRAM_NARROW)) return false;
+    const int64_t T64 = (L.n + 63) / 64, T48 = (L.n + 47) / 48;
+    return int64_t(bt.B) * T64 * (T64 + 1) / 2 < 192 && int64_t(bt.B) * T48 * (T48 + 1) / 2 <= 256;
+}
+
 hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
                        hipStream_t s) {
+    if (use_gram48(L, bt)) {
+        const int T = (L.n + 47) / 48;
+        const dim3 grid(T * (T + 1) / 2, bt.B);
+        float* D2 = L.at<float>(ws, L.D2);
+        int32_t* st = L.at<int32_t>(ws, L.status);
+        int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
+        const int nchunk = (L.d + kGK - 1) / kGK;
+        prof_begin(GLL_K_GRAM, s);
+#define GLL_G48(V, N) \
+    gram48_kernel<V, N><<<grid, 768, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws)
+        if (vec) { if (nchunk >= 4) GLL_G48(true, 4); else if (nchunk >= 2) GLL_G48(true, 2); else GLL_G48(true, 1); }
+        else { if (nchunk >= 4) GLL_G48(false, 4); else if (nchunk >= 2) GLL_G48(false, 2); else GLL_G48(false, 1); }
+#undef GLL_G48
+        prof_end(GLL_K_GRAM, s);
+        return launch_status("knn.hip:launch_gram(48)");
+    }
     if (use_wide_gram(L, bt)) {
         const int T = (L.n + 127) / 128;
         const dim3 grid(T * (T + 1) / 2, bt.B);
