@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
         // lanes own feature columns: accumulate coef_e * x_j in edge order, EB rows of X in
         // flight per batch (padded slots carry coefficient 0 on row i itself)
         const int cnt = min(kWave, end - e0);
-        constexpr int EB = ND <= 2 ? 4 : (ND <= 4 ? 2 : 1);
+        constexpr int EB = ND <= 2 ? 8 : (ND <= 4 ? 4 : (ND <= 8 ? 2 : 1));
         for (int t0 = 0; t0 < cnt; t0 += EB) {
             float s[EB];
             f32x4 v[EB][ND];

@@ -602,6 +602,12 @@ __device__ __forceinline__ int scan_row(const float* __restrict__ row, size_t pl
 #pragma unroll
             for (int p = 1; p < NP; ++p) v[b] += *reinterpret_cast<const f32x4*>(row + p * plane + jc);
         }
+#ifdef GLL_TRACE
+        if (jb == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (blockIdx.x == 0 && threadIdx.x == 0) g_trace[23] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             const int j0 = jb + 4 * (b * kWave + lane);

@@ -191,14 +191,24 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
         }
     }
     if (i >= a.base) {
-        for (int e = 0; e < nlab; ++e) {
-            const int j = ocol[e];
-            const float we = ow[e];
+        // 4 labeled neighbours per step, their label loads all in flight before any is used
+        for (int e0 = 0; e0 < nlab; e0 += 4) {
+            float we[4], yv[4][kMaxCPerLane];
 #pragma unroll
-            for (int q = 0; q < kMaxCPerLane; ++q) {
-                const int c = lane + q * kWave;
-                if (c < a.C) racc[q] += we * yval(Y, j, a.C, c);
+            for (int t = 0; t < 4; ++t) {
+                const bool live = e0 + t < nlab;
+                const int j = ocol[live ? e0 + t : e0];
+                we[t] = live ? ow[e0 + t] : 0.f;
+#pragma unroll
+                for (int q = 0; q < kMaxCPerLane; ++q) {
+                    const int c = lane + q * kWave;
+                    yv[t][q] = c < a.C ? yval(Y, j, a.C, c) : 0.f;
+                }
             }
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int q = 0; q < kMaxCPerLane; ++q) racc[q] += we[t] * yv[t][q];
         }
     }
 #pragma unroll

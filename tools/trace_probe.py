@@ -93,7 +93,7 @@ def timeline(tr, label):
         print(f"gram block 0: shader clock {mhz:.0f} MHz (s_memtime / s_memrealtime)")
     if g[16] and g[20]:
         print("select wave 0: " + ", ".join(f"{nm} +{TICK_US * (g[q] - g[20]):.2f}" for q, nm in
-                                           [(16, "scanned"), (17, "merged"), (18, "refined"),
+                                           [(23, "row loaded"), (16, "scanned"), (17, "merged"), (18, "refined"),
                                             (19, "ranked+written")] if g[q]))
     pts = tr[2][:10].astype(np.int64)
     if pts[0]:
