@@ -391,6 +391,209 @@ __global__ __launch_bounds__(768) void gram48_kernel(const float* __restrict__ X
 }
 
 // --------------------------------------------------------------------------------------
+// K1a (default): split-bf16 Gram on v_mfma_f32_32x32x16_bf16.  Each fp32 feature is split as
+// x = hi + lo with hi = bf16(x), lo = bf16(x - hi), and x.y ~ hi.hi + hi.lo + lo.hi: three
+// bf16 MFMAs at 16x the fp32 MFMA rate (5.3x fewer MFMA cycles than v_mfma_f32_32x32x2_f32).
+// The dropped terms are <= 2^-16 |x_k y_k| each (~1e-6 on the d^2 of unit rows at d = 512,
+// against ~1e-7 for fp32); D2 only nominates the K-1+margin candidates that the select
+// kernel re-ranks with exact fp32 difference-form distances, so the kNN result keeps the
+// fp32 exactness contract.  Row norms come from the fp32 values.
+//
+// 64 x 64 tile per workgroup (upper triangle, mirrored writes), 16 waves.  What bounds a
+// tile at small n is how fast one CU pulls its 2 x 64 rows (256 KiB at d = 512) out of L2,
+// which needs many loads in flight: tools/csrc/load_probe.hip measured 6.9 us for the tile
+// loads with 4 waves x 2 chunks in flight and 4.0 us with 16 waves x 1 chunk.  So:
+//   - features go in phases of 256; in a phase wave w loads rows 16s + w (s = 0..7) of the
+//     128 tile rows (0..63 = rows bi*64.., 64..127 = rows bj*64..), one 1 KiB row segment
+//     per wave instruction (whole lines); two phases of loads are in flight per wave;
+//   - each phase is split into hi / lo bf16 planes in LDS (2 x 128 x 256, row stride 264
+//     bf16: conflict-free ds_read_b128 fragment reads), one barrier, then wave (qd, kq)
+//     multiplies quadrant qd of the tile over feature quarter kq of the phase (4 k-steps x 3
+//     MFMAs into one 32 x 32 accumulator);
+//   - the 4 feature-quarter partials of each quadrant are summed in LDS in a fixed order.
+// --------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+constexpr int kBP = 256;            // features per phase
+constexpr int kBS = kBP + 8;        // LDS plane row stride (bf16)
+
+template <bool VEC>
+__global__ __launch_bounds__(1024) void gram_bf3_kernel(const float* __restrict__ X, int n, int d,
+                                                        int T, float* __restrict__ D2, int ld,
+                                                        int32_t* __restrict__ status,
+                                                        int32_t* __restrict__ rev_cnt,
+                                                        size_t xs, size_t wss) {
+    GLL_TRACE_SCOPE(4);
+    GLL_TRACE_PT(10);
+    X = gshift(X, xs);
+    D2 = gshift(D2, wss);
+    status = gshift(status, wss);
+    rev_cnt = gshift(rev_cnt, wss);
+    // hi plane [128][kBS] then lo plane [128][kBS] (bf16); after the k loop the space holds
+    // the partial quadrants [kq][qd][32][33] and then the finished tile [64][65] (floats)
+    constexpr int kPlane = 128 * kBS;                                   // bf16 per plane
+    __shared__ __attribute__((aligned(16))) __bf16 smem_h[2 * kPlane];
+    __shared__ float sqp[8][16];                                        // [slot][wave]
+    __shared__ float nrm[128];
+    float* smem = reinterpret_cast<float*>(smem_h);
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar row bases
+    const int r = lane & 31, h = lane >> 5;
+    int bi = 0, rem = blockIdx.x;
+    while (rem >= T - bi) {
+        rem -= T - bi;
+        ++bi;
+    }
+    const int bj = bi + rem;
+    {   // per-call reset of the counters the select kernel accumulates into
+        const int g = blockIdx.x * 1024 + tid;
+        if (g < GLL_ST_NWORDS) status[g] = 0;
+        for (int q = g; q < n; q += gridDim.x * 1024) rev_cnt[q] = 0;
+    }
+    const int fo = 4 * lane;   // this lane's 4 features inside a phase
+    auto slot_row = [&](int s) {   // row 16 s + w of the 128 tile rows; rows past n clamped
+        const int R = 16 * s + w;
+        const int row = (R < 64 ? bi * 64 + R : bj * 64 + R - 64);
+        return X + size_t(row < n ? row : n - 1) * d;
+    };
+    const int nph = (d + kBP - 1) / kBP;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    float sq[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) sq[s] = 0.f;
+    const int qd = w & 3, kq = w >> 2;              // MFMA role: quadrant, feature quarter
+    const int qa = qd >> 1, qb = qd & 1;
+
+    auto gload = [&](int ph, f32x4 (&v)[8]) {
+        const int k = ph * kBP + fo;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) v[s] = load4_raw<VEC>(slot_row(s), k, d);
+    };
+    auto phase = [&](int ph, const f32x4 (&v)[8]) {
+        const int k = ph * kBP + fo;
+        __syncthreads();   // the previous phase's fragment reads are done
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const f32x4 f = mask4<VEC>(v[s], k, d);
+            sq[s] += f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+            bf16x4 hv, lv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const __bf16 hb = static_cast<__bf16>(f[e]);
+                hv[e] = hb;
+                lv[e] = static_cast<__bf16>(f[e] - static_cast<float>(hb));
+            }
+            const int o = (16 * s + w) * kBS + fo;
+            *reinterpret_cast<bf16x4*>(smem_h + o) = hv;
+            *reinterpret_cast<bf16x4*>(smem_h + kPlane + o) = lv;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const int kk = 64 * kq + 16 * st + 8 * h;
+            const int oa = (32 * qa + r) * kBS + kk, ob = (64 + 32 * qb + r) * kBS + kk;
+            const bf16x8 ha = *reinterpret_cast<const bf16x8*>(smem_h + oa);
+            const bf16x8 la = *reinterpret_cast<const bf16x8*>(smem_h + kPlane + oa);
+            const bf16x8 hb = *reinterpret_cast<const bf16x8*>(smem_h + ob);
+            const bf16x8 lb = *reinterpret_cast<const bf16x8*>(smem_h + kPlane + ob);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(la, hb, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha, lb, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha, hb, acc, 0, 0, 0);
+        }
+    };
+    {
+        f32x4 va[8], vb[8];
+        gload(0, va);
+        for (int ph = 0; ph < nph; ph += 2) {
+            gload(ph + 1 < nph ? ph + 1 : ph, vb);   // unconditional: static vmcnt counts
+#ifdef GLL_TRACE
+            if (ph == 0) {
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                GLL_TRACE_PT(15);
+            }
+#endif
+            phase(ph, va);
+            if (ph + 1 >= nph) break;
+            gload(ph + 2 < nph ? ph + 2 : ph + 1, va);
+            phase(ph + 1, vb);
+        }
+    }
+    GLL_TRACE_PT(12);
+    // row norms: slot s of wave w is tile row 16 s + w, its features spread over the wave
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const float t = wave_sum_dpp(sq[s]);
+        if (lane == 0) sqp[s][w] = t;
+    }
+    __syncthreads();   // fragment reads done: the planes become partial / tile space
+    // partial quadrant -> LDS part[kq][qd][32][33] (C layout: col = lane & 31,
+    // row = (e&3) + 8(e>>2) + 4h)
+    float* pw = smem + (kq * 4 + qd) * 32 * 33;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) pw[((e & 3) + 8 * (e >> 2) + 4 * h) * 33 + r] = acc[e];
+    if (tid < 128) nrm[tid] = sqp[tid >> 4][tid & 15];
+    __syncthreads();
+    // tile element (ti, tj..tj+3): sum of the 4 feature quarters, fixed order
+    const int ti = tid >> 4, tj = 4 * (tid & 15);
+    float v[4];
+    {
+        const int q = 2 * (ti >> 5) + (tj >> 5), rr = ti & 31;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int cc = (tj & 31) + e;
+            float t = 0.f;
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) t += smem[(k4 * 4 + q) * 32 * 33 + rr * 33 + cc];
+            v[e] = t;
+        }
+    }
+    __syncthreads();
+    float* tile = smem + 16 * 32 * 33;   // [64][65], past the partials
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[ti * 65 + tj + e] = nrm[ti] + nrm[64 + tj + e] - 2.f * v[e];
+    __syncthreads();
+    GLL_TRACE_PT(13);
+    // direct orientation: row bi*64 + ti, columns bj*64 + tj .. +3; a diagonal tile takes the
+    // upper triangle for both halves so D2 stays bitwise symmetric
+    const int i = bi * 64 + ti;
+    if (i < n) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int jj = tj + e;
+            o[e] = (bi == bj && jj < ti) ? tile[jj * 65 + ti] : tile[ti * 65 + jj];
+        }
+        float* dst = D2 + size_t(i) * ld + bj * 64 + tj;
+        if (bj * 64 + tj + 4 <= n) {
+            *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (bj * 64 + tj + e < n) dst[e] = o[e];
+        }
+    }
+    // mirrored orientation: row bj*64 + ti, columns bi*64 + tj .. +3 from the tile's column ti
+    const int jr = bj * 64 + ti;
+    if (bi != bj && jr < n) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = tile[(tj + e) * 65 + ti];
+        float* dst = D2 + size_t(jr) * ld + bi * 64 + tj;
+        if (bi * 64 + tj + 4 <= n) {
+            *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (bi * 64 + tj + e < n) dst[e] = o[e];
+        }
+    }
+    GLL_TRACE_PT(14);
+}
+
+// --------------------------------------------------------------------------------------
 // K1a': wide symmetric Gram tile for large problems (many tiles): 128 x 128 per workgroup, 4
 // waves each owning a 64 x 64 sub-tile as 2 x 2 independent 32 x 32 MFMA accumulators (one
 // A fragment feeds two MFMAs, four chains keep the MFMA pipe full from one wave per SIMD),
@@ -827,6 +1030,20 @@ static bool use_gram48(const Layout& L, const Batch& bt) {
 
 hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
                        hipStream_t s) {
+    if (L.KS == 1 && !(L.flags & GLL_FLAG_GRAM_F32)) {
+        const int T = (L.n + 63) / 64;
+        const dim3 grid(T * (T + 1) / 2, bt.B);
+        float* D2 = L.at<float>(ws, L.D2);
+        int32_t* st = L.at<int32_t>(ws, L.status);
+        int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
+        prof_begin(GLL_K_GRAM, s);
+        if (vec)
+            gram_bf3_kernel<true><<<grid, 1024, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
+        else
+            gram_bf3_kernel<false><<<grid, 1024, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
+        prof_end(GLL_K_GRAM, s);
+        return launch_status("knn.hip:launch_gram(bf3)");
+    }
     if (use_gram48(L, bt)) {
         const int T = (L.n + 47) / 48;
         const dim3 grid(T * (T + 1) / 2, bt.B);

@@ -75,6 +75,65 @@ __device__ __forceinline__ void block_sum2(float& a, float& b, float* red, int& 
 }
 
 
+// Block-wide sum of three values in one LDS exchange (the single-reduction CG).  Partials
+// are laid out [value][wave] so each total is read with 16-B loads; fixed order everywhere.
+template <int NT>
+__device__ __forceinline__ void block_sum3(float& a, float& b, float& c, float* red, int& phase) {
+    a = dpp_add<0xB1, 0xf>(a); b = dpp_add<0xB1, 0xf>(b); c = dpp_add<0xB1, 0xf>(c);
+    a = dpp_add<0x4E, 0xf>(a); b = dpp_add<0x4E, 0xf>(b); c = dpp_add<0x4E, 0xf>(c);
+    a = dpp_add<0x141, 0xf>(a); b = dpp_add<0x141, 0xf>(b); c = dpp_add<0x141, 0xf>(c);
+    a = dpp_add<0x140, 0xf>(a); b = dpp_add<0x140, 0xf>(b); c = dpp_add<0x140, 0xf>(c);
+    a = dpp_add<0x142, 0xa>(a); b = dpp_add<0x142, 0xa>(b); c = dpp_add<0x142, 0xa>(c);
+    a = dpp_add<0x143, 0xc>(a); b = dpp_add<0x143, 0xc>(b); c = dpp_add<0x143, 0xc>(c);
+    if constexpr (NT == kWave) {
+        a = readlane_f(a, 63);
+        b = readlane_f(b, 63);
+        c = readlane_f(c, 63);
+    } else {
+        constexpr int NW = NT / kWave;
+        constexpr int NQ = NW < 4 ? 4 : NW;          // 16-B rows
+        float* q = red + phase * 3 * NQ;
+        phase ^= 1;
+        if (lane_id() == 63) {
+            const int w = threadIdx.x >> 6;
+            q[w] = a;
+            q[NQ + w] = b;
+            q[2 * NQ + w] = c;
+        }
+        __syncthreads();
+        a = b = c = 0.f;
+        if constexpr (NW % 4 == 0) {
+#pragma unroll
+            for (int w = 0; w < NW; w += 4) {
+                const f32x4 va = *reinterpret_cast<const f32x4*>(q + w);
+                const f32x4 vb = *reinterpret_cast<const f32x4*>(q + NQ + w);
+                const f32x4 vc = *reinterpret_cast<const f32x4*>(q + 2 * NQ + w);
+                a += va.x; a += va.y; a += va.z; a += va.w;
+                b += vb.x; b += vb.y; b += vb.z; b += vb.w;
+                c += vc.x; c += vc.y; c += vc.z; c += vc.w;
+            }
+        } else {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                a += q[w];
+                b += q[NQ + w];
+                c += q[2 * NQ + w];
+            }
+        }
+    }
+}
+
+// Wave-uniform maximum of a small non-negative int (setup only).
+__device__ __forceinline__ int wave_max_int(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int o = __shfl_xor(v, off);
+        v = o > v ? o : v;
+    }
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+
 // Exclusive prefix sum of one int per thread over the block; `total` gets the block sum.
 template <int NT>
 __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int& total) {
@@ -105,7 +164,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int& total) 
     }
 }
 
-template <int NT, int R, int S, typename TB>
+template <int NT, int R, int S, typename TB, bool CGC>
 __global__ __launch_bounds__(NT) void cg_ell_kernel(
     int m, int C, int base, const int32_t* __restrict__ row_start,
     const int32_t* __restrict__ row_len, const int32_t* __restrict__ ucnt,
@@ -131,8 +190,8 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     st_iters = gshift(st_iters, sts);
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
-    float* red = smem;                                  // 4 x 16 floats of reduction scratch
-    int* scan = reinterpret_cast<int*>(smem + 64);      // 16 ints of scan scratch
+    float* red = smem;                                  // 96 floats of reduction scratch
+    int* scan = reinterpret_cast<int*>(smem + 96);      // 16 ints of scan scratch
     float* P_ = smem + 128;                             // search direction (gathered)
     int* lcol = reinterpret_cast<int*>(P_ + ((m + 3) & ~3));   // overflow entries, compacted
     float* lw = reinterpret_cast<float*>(lcol + mat_cap);
@@ -206,11 +265,107 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     GLL_TRACE_PT(2);
     int phase = 0;
     if constexpr (NT > kWave) __syncthreads();
+    int it = 0;
+    bool conv;
+    if constexpr (CGC) {
+        // Chronopoulos-Gear single-reduction PCG: one fused (r.u, w.u, r.r) exchange and one
+        // publish barrier per iteration (classic PCG: two exchanges + publish = 3 barriers).
+        // s = A p by recurrence; u = M^-1 r is what is published and multiplied.
+        // Each wave gathers only the ELL slots some row of its own holds (wave-uniform bound
+        // in groups of 4: rows average ~6 of the 24 slots at NS).
+        int smax[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int u = tid + NT * q;
+            const int len = u < m ? ucnt[u] : 0;
+            smax[q] = wave_max_int(len < S ? len : S);
+        }
+        auto spmv = [&](int q, float pq) {
+            float pv[S];
+#pragma unroll
+            for (int s0 = 0; s0 < S; s0 += 4) {
+                if (s0 < smax[q]) {
+#pragma unroll
+                    for (int t = 0; t < 4 && s0 + t < S; ++t) pv[s0 + t] = P_[ec[q][s0 + t]];
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 4 && s0 + t < S; ++t) pv[s0 + t] = 0.f;
+                }
+            }
+            float acc = 0.f;
+#pragma unroll
+            for (int s2 = 0; s2 < S; ++s2) acc += ew[q][s2] * pv[s2];
+            if (matl) {
+                for (int t = 0; t < olen[q]; ++t) {
+                    const int e = ost[q] + t;
+                    acc += lw[e] * P_[lcol[e]];
+                }
+            } else {
+                for (int t = 0; t < olen[q]; ++t) {
+                    const int e = ost[q] + t;
+                    acc += wv[e] * P_[col[e] - base];
+                }
+            }
+            return dg[q] * pq - acc;   // (Luu u)_row = (deg + tau) u_row - sum_j W_rowj u_j
+        };
+        // pre-step: w0 = A u0 (u0 = p, already published), gamma0 = (r,u), delta0 = (w,u)
+        float sv[R];
+        float dl = 0.f;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            sv[q] = spmv(q, p[q]);
+            dl += p[q] * sv[q];
+        }
+        block_sum3<NT>(rz, bb, dl, red, phase);
+        GLL_TRACE_PT(3);
+        const float tol2 = rtol * rtol * bb;
+        conv = !(bb > 0.f);
+        float gam = rz;
+        float alpha = dl > 0.f ? gam / dl : 0.f;
+        if (!(dl > 0.f)) alpha = -1.f;   // breakdown before the first step
+        while (!conv && alpha > 0.f && it < max_iter) {
+            ++it;
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                x[q] += alpha * p[q];
+                r[q] -= alpha * sv[q];
+                ap[q] = mi[q] * r[q];                       // u = M^-1 r
+                const int u = tid + NT * q;
+                if (u < m) P_[u] = ap[q];
+            }
+            if constexpr (NT > kWave) __syncthreads();
+            if (it == 1) GLL_TRACE_PT(4);
+            float gn = 0.f, de = 0.f, rr = 0.f;
+            float w[R];
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                w[q] = spmv(q, ap[q]);
+                gn += r[q] * ap[q];
+                de += w[q] * ap[q];
+                rr += r[q] * r[q];
+            }
+            block_sum3<NT>(gn, de, rr, red, phase);
+            if (it == 1) GLL_TRACE_PT(6);
+            if (rr <= tol2) {
+                conv = true;
+                break;
+            }
+            const float beta = gn / gam;
+            const float den = de - beta * gn / alpha;
+            if (!(den > 0.f)) break;   // breakdown or NaN: reported as non-converged
+            alpha = gn / den;
+            gam = gn;
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                p[q] = ap[q] + beta * p[q];
+                sv[q] = w[q] + beta * sv[q];
+            }
+        }
+    } else {
     block_sum2<NT>(rz, bb, red, phase);
     GLL_TRACE_PT(3);
     const float tol2 = rtol * rtol * bb;
-    int it = 0;
-    bool conv = !(bb > 0.f);
+    conv = !(bb > 0.f);
     while (!conv && it < max_iter) {
         ++it;
         float pap = 0.f, unused = 0.f;
@@ -263,6 +418,7 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
         }
         if constexpr (NT > kWave) __syncthreads();
         if (it == 1) GLL_TRACE_PT(7);
+    }
     }
     GLL_TRACE_PT(8);
 #pragma unroll
@@ -371,7 +527,7 @@ __global__ __launch_bounds__(NT) void cg_lds_kernel(
 }
 
 
-template <int NT, int R, int S, typename TB>
+template <int NT, int R, int S, typename TB, bool CGC>
 static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* b, size_t bs,
                           double* out64, float* out32, float rtol, int max_iter,
                           int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
@@ -391,7 +547,7 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
         if (getenv("GLL_DEBUG")) fprintf(stderr, "gll: run_ell S=%d but ELL width %d\n", S, L.SE);
         return hipErrorInvalidValue;
     }
-    auto fn = cg_ell_kernel<NT, R, S, TB>;
+    auto fn = cg_ell_kernel<NT, R, S, TB, CGC>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
     fn<<<dim3(L.C, bt.B), NT, lds, s>>>(
         L.m, L.C, L.base, L.at<int32_t>(ws, L.row_start), L.at<int32_t>(ws, L.row_len),
@@ -410,19 +566,26 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     // per-column register kernels' sweet spot (m > 1024: their ELL slices overflow); measured
     // at stress (m 4096, K 30): 209 us against 288 us per solve.  Batches keep the
     // per-column kernels (B x C workgroups already fill the GPU).
-    if (bt.B == 1 && L.C <= 16 && (m > 1024 || (L.flags & GLL_FLAG_CG_GRID))) {
+    if (bt.B == 1 && L.C <= 16 && !(L.flags & GLL_FLAG_CG_PERCOL) &&
+        (m > 1024 || (L.flags & GLL_FLAG_CG_GRID))) {
         const int b_dtype = sizeof(TB) == 8 ? GLL_DT_F64 : GLL_DT_F32;
         return launch_cg_grid_luu(L, ws, b, b_dtype, out64, out32, rtol, 0.f, max_iter,
                                   st_nonconv, st_iters, s);
     }
-#define GLL_ELL(NT, R, S)                                                                   \
-    return run_ell<NT, R, S, TB>(L, bt, ws, b, bs, out64, out32, rtol, max_iter, st_nonconv, \
-                                 st_iters, s)
+#define GLL_ELL(NT, R, S)                                                                     \
+    return (L.flags & GLL_FLAG_CG_CLASSIC)                                                    \
+               ? run_ell<NT, R, S, TB, false>(L, bt, ws, b, bs, out64, out32, rtol, max_iter, \
+                                              st_nonconv, st_iters, s)                        \
+               : run_ell<NT, R, S, TB, true>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,  \
+                                             st_nonconv, st_iters, s)
     if (m <= 64) GLL_ELL(64, 1, 24);
     if (m <= 128) GLL_ELL(128, 1, 24);
     if (m <= 256) GLL_ELL(256, 1, 24);
     // m <= 512: one row per thread is the lower latency for a single graph; batches run more
     // workgroups per CU with 4 waves x 2 rows (B = 64: 44.7 -> 36.6 us per launch)
+    static const int cg_nt = getenv("GLL_CG_NT") ? atoi(getenv("GLL_CG_NT")) : 0;  // diagnostic
+    if (m <= 512 && cg_nt == 128) GLL_ELL(128, 4, 24);
+    if (m <= 512 && cg_nt == 256) GLL_ELL(256, 2, 24);
     if (m <= 512 && bt.B == 1) GLL_ELL(512, 1, 24);
     if (m <= 512) GLL_ELL(256, 2, 24);
     if (m <= 1024) GLL_ELL(1024, 1, 16);

@@ -285,9 +285,13 @@ def _synth_batch(cfg, B, seed0=0):
     return np.stack(Xs), np.stack(Ys), c
 
 
-@pytest.mark.parametrize("cfg,eps,ydt", [("plumbing", "auto", "i64"), ("ns", 1.0, "f32")])
-def test_batched_graphs_equal_single_calls_bitwise(cfg, eps, ydt):
-    """B graphs in one launch per kernel give exactly B single calls."""
+@pytest.mark.parametrize("cfg,eps,ydt,exact", [("plumbing", "auto", "i64", True),
+                                               ("ns", 1.0, "f32", False)])
+def test_batched_graphs_equal_single_calls_bitwise(cfg, eps, ydt, exact):
+    """B graphs in one launch per kernel give B single calls.  Bitwise where
+    the batched launch runs the same CG configuration as the single one (plumbing); at NS
+    batches run the 256x2 per-column CG (solve.hip cg_dispatch), whose dot-product order
+    differs, so there the bar is 1e-5 relative (10x below the 1e-4 parity bar)."""
     from graphlearninglayer_amd.synth import seeded_gbar
     GLL = _gll()
     B = 5
@@ -301,8 +305,12 @@ def test_batched_graphs_equal_single_calls_bitwise(cfg, eps, ydt):
     Ub.backward(torch.from_numpy(G).cuda())
     for g in range(B):
         U1, gx1 = _run(Xs[g], Ys[g], 0.07, eps, c["k"], G[g])
-        np.testing.assert_array_equal(Ub[g].detach().cpu().numpy(), U1)
-        np.testing.assert_array_equal(Xb.grad[g].cpu().numpy(), gx1)
+        if exact:
+            np.testing.assert_array_equal(Ub[g].detach().cpu().numpy(), U1)
+            np.testing.assert_array_equal(Xb.grad[g].cpu().numpy(), gx1)
+        else:
+            assert O.rel_err(Ub[g].detach().cpu().numpy(), U1) <= 1e-5
+            assert O.rel_err(Xb.grad[g].cpu().numpy(), gx1) <= 1e-5
 
 
 def test_batched_shared_labels_python_and_cpp_paths_agree():

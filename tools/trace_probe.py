@@ -21,7 +21,7 @@ TICK_US = 0.01
 lib = ct.CDLL(os.path.join(ROOT, "graphlearninglayer_amd", "_obj", "libgll_trace.so"))
 lib.gll_workspace_bytes.restype = ct.c_size_t
 lib.gll_trace_read.argtypes = [ct.c_int, ct.POINTER(ct.c_ulonglong)]
-UNITS = {0: ("knn", ["gram", "select", "gram_wide", "gram48"]), 1: ("rows", ["row_build"]),
+UNITS = {0: ("knn", ["gram", "select", "gram_wide", "gram48", "gram_bf3"]), 1: ("rows", ["row_build"]),
          2: ("solve", ["cg_ell", "cg_lds", "cg_csr"]), 3: ("grad", ["edge_coef", "grad_spmm"])}
 CG_PTS = ["entry", "ell loaded+P", "ovf compacted", "rz/bb reduced", "it1 spmv", "it1 pAp",
           "it1 rr", "it1 P published", "loop done", "stored"]
