@@ -6,7 +6,8 @@
 One step = one `LaplaceLearningSparseHard.apply` forward (kNN graph built from scratch)
 + the backward of a fixed seeded upstream gradient dL/dU, on the rank's own synthetic
 minibatch graph (seed = rank; SURVEY.md §8d generator), plus the asynchronous RCCL
-all_gather of the predictions U that the sharded path performs (§8e).  Inputs are resident
+all_gather of the predictions U that the sharded path performs (§8e), coalesced over
+GATHER_EVERY calls.  Inputs are resident
 in HBM before timing starts.  Rank 0 prints ONE JSON line; `value` = calls/s over all ranks.
 """
 from __future__ import annotations
@@ -26,13 +27,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from graphlearninglayer_amd import GLL, _lib  # noqa: E402
-from graphlearninglayer_amd.parallel import gather_predictions, shard_rank_seed  # noqa: E402
+from graphlearninglayer_amd.parallel import PredictionGatherer, shard_rank_seed  # noqa: E402
 from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth  # noqa: E402
 
 METRIC = "GLL fwd+bwd calls/sec (base=500,batch=500,d=512,k=10) at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 MFMA_F32_PEAK_TFS = 157.3    # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), spec
 PROF_PERIOD = 8              # event-bracket every 8th launch of the dominant kernel
+GATHER_EVERY = 8             # calls per coalesced all_gather of the predictions
 EPS = {"plumbing": 1.0, "ns": 1.0, "fullysup": 1.0, "stress": "auto"}
 TAU = {"plumbing": 0.07, "ns": 0.07, "fullysup": 0.07, "stress": 0.07}
 
@@ -71,7 +73,7 @@ def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps):
 
 
 # C-ABI kernel ids (gll_kernel_name) -> device symbols as rocprofv3 names them
-PMC_SYMBOLS = {"gram_d2_kernel": ["gram_lds_kernel"], "knn_select_kernel": ["knn_select_kernel"],
+PMC_SYMBOLS = {"gram_d2_kernel": ["gram_bf3_kernel", "gram48_kernel", "gram_lds_kernel"], "knn_select_kernel": ["knn_select_kernel"],
                "row_build_kernel": ["row_build_kernel"],
                "cg_kernel": ["cg_ell_kernel", "cg_lds_kernel"],
                "edge_coef_kernel": ["edge_coef_kernel"], "grad_spmm_kernel": ["grad_spmm_kernel"]}
@@ -140,6 +142,43 @@ def batched_measure(c, eps, tau, k, B, units, dev, rank, steps=20, warmup=5):
                          "launches": cnt}}
 
 
+def c_abi_measure(X, Y, tau, eps, k, gbar, steps, warmup):
+    """The same fwd+bwd through the C ABI of include/gll.h (gll_forward + gll_backward on the
+    current stream, caller-owned workspace) without torch's autograd engine in the loop: what a
+    native caller of the boundary gets, and the GPU-side rate of the step."""
+    import ctypes as ct
+
+    n, d = X.shape
+    base, C = Y.shape
+    prob = GLL.make_problem(n, d, base, C, k, tau, eps)
+    lib = _lib.lib()
+    ws = torch.empty(lib.gll_workspace_bytes(ct.byref(prob)), dtype=torch.uint8, device=X.device)
+    U = torch.empty(n - base, C, dtype=torch.float64, device=X.device)
+    gx = torch.empty(n, d, dtype=torch.float32, device=X.device)
+    X32 = X.detach().contiguous()
+    Yc = Y.contiguous()
+    s = torch.cuda.current_stream(X.device).cuda_stream
+    pp = ct.byref(prob)
+    xp, yp, wp, up, gp, gxp = (X32.data_ptr(), Yc.data_ptr(), ws.data_ptr(), U.data_ptr(),
+                               gbar.data_ptr(), gx.data_ptr())
+
+    def step():
+        lib.gll_forward(pp, xp, yp, _lib.GLL_DT_F32, wp, up, s)
+        lib.gll_backward(pp, xp, None, 0, wp, gp, _lib.GLL_DT_F64, gxp, s)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value": round(steps / el, 3), "unit": "calls/s", "ms_per_step": round(1e3 * el / steps, 4),
+            "note": "same kernels and inputs through gll_forward + gll_backward (include/gll.h), "
+                    "no torch autograd engine on the host path"}
+
+
 def cpu_baseline(cfg, eps, tau, seconds):
     """Time the reference's CPU step sequence (oracle/gll_port.py, 'port') on this host."""
     from oracle import gll_port
@@ -184,16 +223,17 @@ def main():
     gbar = torch.from_numpy(seeded_gbar(c["batch"], 10, 1234 + rank)).to(dev)
     lap = GLL.LaplaceLearningSparseHard.apply
 
+    gatherer = PredictionGatherer(every=GATHER_EVERY)
+
     def step():
         U = lap(X, Y, tau, eps, k)
-        _, work = gather_predictions(U, async_op=True)
+        gatherer.add(U)          # one async RCCL all_gather per GATHER_EVERY calls
         (gx,) = torch.autograd.grad(U, X, gbar)
-        if work is not None:
-            work.wait()
         return U, gx
 
     for _ in range(a.warmup):
         step()
+    gatherer.wait()
     torch.cuda.synchronize()
 
     # which kernel dominates: one untimed instrumented pass over all kernels
@@ -205,6 +245,7 @@ def main():
             _lib.prof_enable(q, 1)
         for _ in range(10):
             step()
+        gatherer.wait()
         torch.cuda.synchronize()
         for q in range(_lib.K_COUNT):
             ms, cnt = _lib.prof_read(q)
@@ -224,6 +265,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         U, gx = step()
+    gatherer.wait()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -266,6 +308,10 @@ def main():
             b_, w_ = units[kn]
             v["algorithmic"] = (f"{w_ / 1e9:.4g} GFLOP" if b_ == "mfma" else f"{w_ / 1e6:.4g} MB")
 
+    c_abi = None
+    if not a.no_profile:
+        c_abi = c_abi_measure(X, Y, tau, eps, k, gbar, a.steps, a.warmup)
+
     batched = None
     if a.batch > 0 and roofline is not None:
         batched = batched_measure(c, eps, tau, k, a.batch, units, dev, rank)
@@ -292,10 +338,12 @@ def main():
             "config": {"workload": a.config, "base": c["base"], "batch": c["batch"], "d": c["d"],
                        "k": k, "eps": eps, "tau": tau, "classes": 10,
                        "parallelism": f"dp{world}", "upstream_grad": "fixed seeded dL/dU",
-                       "collective": "all_gather(U) per step" if world > 1 else "none"},
+                       "collective": (f"async all_gather(U) over RCCL, one per {GATHER_EVERY} calls"
+                                      if world > 1 else "none")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels": per_kernel,
+            "c_abi": c_abi,
             "batched": batched,
         }
         if roofline is not None:

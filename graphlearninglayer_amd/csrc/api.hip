@@ -125,7 +125,7 @@ static int build_graph(const gll_problem* p, const Layout& L, const Batch& bt, c
     if (launch_select(L, bt, ws, X, p->eps, auto_eps, vec, public_status(p, L, ws), s) !=
         hipSuccess)
         return GLL_ERR_HIP;
-    return hip_status(launch_finalize(L, bt, ws, Y, y_dtype, p->tau, s));
+    return hip_status(launch_finalize(L, bt, ws, Y, y_dtype, p->tau, auto_eps ? 0.f : p->eps, s));
 }
 
 static int forward_impl(const gll_problem* p, int B, const float* X, const void* Y, int y_dtype,
@@ -169,7 +169,8 @@ static int backward_impl(const gll_problem* p, int B, const float* X, void* ws,
                                  st + GLL_ST_BWD_NONCONV, st + GLL_ST_BWD_ITERS, s);
     if (e != hipSuccess) return GLL_ERR_HIP;
     const bool auto_eps = !(p->eps > 0.f);
-    return hip_status(launch_backward_grad(L, bt, ws, X, auto_eps, gradX, vec_ok(X, p->d), s));
+    return hip_status(launch_backward_grad(L, bt, ws, X, auto_eps, p->eps, gradX,
+                                           vec_ok(X, p->d), s));
 }
 
 }  // namespace gll

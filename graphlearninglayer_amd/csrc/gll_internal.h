@@ -361,7 +361,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
                          float eps_fixed, bool auto_eps, bool vec, int32_t* status_pub,
                          hipStream_t s);
 hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,
-                           int y_dtype, float tau, hipStream_t s);
+                           int y_dtype, float tau, float eps_fixed, hipStream_t s);
 // b: right-hand sides of graph 0, `b_stride` bytes apart (the workspace rhs or gbar)
 hipError_t launch_cg_luu(const Layout& L, const Batch& bt, void* ws, const void* b,
                          size_t b_stride, int b_dtype, double* out64, float* out32, float rtol,
@@ -378,6 +378,7 @@ hipError_t launch_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* co
                          const float* val, const float* b, float* x, float atol, int max_iter,
                          int32_t* iters, int32_t* nonconv, float* gvec, hipStream_t s);
 hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, const float* X,
-                                bool auto_eps, float* gradX, bool vec, hipStream_t s);
+                                bool auto_eps, float eps_fixed, float* gradX, bool vec,
+                                hipStream_t s);
 
 }  // namespace gll

@@ -881,7 +881,7 @@ __device__ __forceinline__ bool merge_fast(uint64_t (&key)[KS], int kc, int seen
     return __ballot(popped == KS && seen > KS) != 0;
 }
 
-template <int KC, bool VEC, int NP>
+template <int KC, bool VEC, int NP, int PG>
 __global__ __launch_bounds__(256) void knn_select_kernel(
     const float* __restrict__ D2, int ld, size_t plane, const float* __restrict__ X, int n, int d, int K,
     int kc, float eps_fixed, int auto_eps, int RCAP, int32_t* __restrict__ knn_idx,
@@ -922,40 +922,55 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
             ci = merge_exact<KC>(full, kc);
         }
     }
-    // 3) exact squared distances, 8 candidates per pass (8 lanes each, across d).  (Two
-    //    groups per sweep -- every load in flight at once -- saved ~0.2 us at NS but took 191
-    //    VGPRs; with B graphs or large n the lost occupancy cost 20-45%: kept one group.)
+    // 3) exact squared distances, 8 candidates per pass (8 lanes each, across d).  PG passes
+    //    per sweep with every load in flight at once: PG = 2 for single-graph launches (one
+    //    wave per SIMD anyway); batches keep PG = 1 (191 VGPRs at PG = 2 cost them 20-45%
+    //    occupancy).  Per-candidate arithmetic is the same either way.
     const int grp = lane >> 3, sub = lane & 7;
     const float* xi = X + size_t(i) * d;
     float ce = __builtin_inff();
-    for (int p0 = 0; p0 < kc; p0 += 8) {
-        const int j = __shfl(ci, p0 + grp < kc ? p0 + grp : 0);
-        const bool live = p0 + grp < kc && j >= 0;
-        const float* xj = X + size_t(live ? j : i) * d;
-        float part = 0.f;
+    for (int p0 = 0; p0 < kc; p0 += 8 * PG) {
+        const float* xj[PG];
+#pragma unroll
+        for (int g2 = 0; g2 < PG; ++g2) {
+            const int idx = p0 + 8 * g2 + grp;
+            const int j = __shfl(ci, idx < kc ? idx : 0);
+            const bool live = idx < kc && j >= 0;
+            xj[g2] = X + size_t(live ? j : i) * d;
+        }
+        float part[PG];
+#pragma unroll
+        for (int g2 = 0; g2 < PG; ++g2) part[g2] = 0.f;
         for (int kb = 0; kb < d; kb += 512) {   // 16 steps of 32 features: all loads in flight
-            f32x4 va[16], vb[16];
+            f32x4 va[16], vb[PG][16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) {   // straight-line: every load issued before use
                 const int k = kb + 32 * u + 4 * sub;
                 va[u] = load4_raw<VEC>(xi, k, d);
-                vb[u] = load4_raw<VEC>(xj, k, d);
+#pragma unroll
+                for (int g2 = 0; g2 < PG; ++g2) vb[g2][u] = load4_raw<VEC>(xj[g2], k, d);
             }
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {   // same order from either end: symmetric in (i, j)
-                const int k = kb + 32 * u + 4 * sub;
-                const f32x4 df = mask4<VEC>(va[u] - vb[u], k, d);
-                part += df.x * df.x;
-                part += df.y * df.y;
-                part += df.z * df.z;
-                part += df.w * df.w;
+            for (int g2 = 0; g2 < PG; ++g2) {
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {   // same order from either end: symmetric in (i, j)
+                    const int k = kb + 32 * u + 4 * sub;
+                    const f32x4 df = mask4<VEC>(va[u] - vb[g2][u], k, d);
+                    part[g2] += df.x * df.x;
+                    part[g2] += df.y * df.y;
+                    part[g2] += df.z * df.z;
+                    part[g2] += df.w * df.w;
+                }
             }
         }
-        part = group8_sum(part);
 #pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            const float v = readlane_f(part, 8 * g);
-            if (lane == p0 + g) ce = v;
+        for (int g2 = 0; g2 < PG; ++g2) {
+            const float tot = group8_sum(part[g2]);
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const float v = readlane_f(tot, 8 * g);
+                if (lane == p0 + 8 * g2 + g) ce = v;
+            }
         }
     }
     GLL_TRACE_PT(18);
@@ -1122,7 +1137,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     prof_begin(GLL_K_SELECT, s);
     const size_t plane = size_t(n) * L.ldD;
 #define GLL_SEL3(KCV, V, NPV)                                                                  \
-    knn_select_kernel<KCV, V, NPV><<<grid, 256, 0, s>>>(                                       \
+    (bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2> : knn_select_kernel<KCV, V, NPV, 1>)<<<grid, 256, 0, s>>>( \
         L.at<float>(ws, L.D2), L.ldD, plane, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0,     \
         L.RCAP,                                                                                \
         L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \

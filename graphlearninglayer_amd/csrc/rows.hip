@@ -26,6 +26,7 @@ struct RowArgs {
     int n, base, C, K, RCAP, Wcap;
     int64_t bump_base;
     float tau;
+    float eps_fixed;   // > 0: fixed epsilon, no eps gathers
     const int32_t* knn_idx;
     const float* knn_d2;
     const int32_t* rev_cnt;
@@ -89,8 +90,9 @@ __device__ __forceinline__ float yval(const TY* Y, int j, int C, int c) {
 template <bool LDS, typename TY>
 __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict__ Y, int i,
                                           int start, int fi, float fd, bool fval,
-                                          uint64_t fmask, int nf, int rc, int* s_col,
-                                          float* s_d2, int* t_col, float* t_d2, float* t_w) {
+                                          uint64_t fmask, int nf, int rc, float ei,
+                                          int* s_col, float* s_d2, int* t_col, float* t_d2,
+                                          float* t_w) {
     const int lane = lane_id();
     int* scol = LDS ? s_col : a.tmp_col + start;
     float* sd2 = LDS ? s_d2 : a.tmp_d2 + start;
@@ -156,13 +158,13 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
     }
     if constexpr (!LDS) __threadfence();
     // sorted pass: weights, degree, labeled-prefix length
-    const float ei = a.eps[i];
     float dsum = 0.f;
     int nlab = 0;
     for (int e = lane; e < L; e += kWave) {
         const int c = ocol[e];
         const float dd = od2[e];
-        const float we = expf(-4.f * dd / (ei * a.eps[c]));   // GLL.py:216/233
+        const float ec = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[c];
+        const float we = expf(-4.f * dd / (ei * ec));   // GLL.py:216/233
         ow[e] = we;
         if constexpr (LDS) {
             a.col[start + e] = c;
@@ -191,11 +193,11 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
         }
     }
     if (i >= a.base) {
-        // 4 labeled neighbours per step, their label loads all in flight before any is used
-        for (int e0 = 0; e0 < nlab; e0 += 4) {
-            float we[4], yv[4][kMaxCPerLane];
+        // 8 labeled neighbours per step, their label loads all in flight before any is used
+        for (int e0 = 0; e0 < nlab; e0 += 8) {
+            float we[8], yv[8][kMaxCPerLane];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < 8; ++t) {
                 const bool live = e0 + t < nlab;
                 const int j = ocol[live ? e0 + t : e0];
                 we[t] = live ? ow[e0 + t] : 0.f;
@@ -206,7 +208,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
                 }
             }
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
+            for (int t = 0; t < 8; ++t)
 #pragma unroll
                 for (int q = 0; q < kMaxCPerLane; ++q) racc[q] += we[t] * yv[t][q];
         }
@@ -260,6 +262,7 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
     const uint64_t fmask = __ballot(fval);
     const int nf = __popcll(fmask);
     const int rc = a.rev_cnt[i];
+    const float ei = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[i];   // issued with the lists
     const int lbound = nf + rc;
     int start = i * a.Wcap;
     if (lbound > a.Wcap) {
@@ -268,15 +271,15 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
         start = readlane_i(s0, 0);
     }
     if (lbound <= kStage)
-        build_row<true, TY>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, s_col[wv], s_d2[wv],
-                            t_col[wv], t_d2[wv], t_w[wv]);
+        build_row<true, TY>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, ei, s_col[wv],
+                            s_d2[wv], t_col[wv], t_d2[wv], t_w[wv]);
     else
-        build_row<false, TY>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, nullptr, nullptr,
+        build_row<false, TY>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, ei, nullptr, nullptr,
                              nullptr, nullptr, nullptr);
 }
 
 hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,
-                           int y_dtype, float tau, hipStream_t s) {
+                           int y_dtype, float tau, float eps_fixed, hipStream_t s) {
     if (L.C > kMaxCPerLane * kWave) return hipErrorInvalidValue;
     RowArgs a;
     a.n = L.n;
@@ -287,6 +290,7 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     a.Wcap = L.Wcap;
     a.bump_base = int64_t(L.n) * L.Wcap;
     a.tau = tau;
+    a.eps_fixed = eps_fixed;
     a.knn_idx = L.at<int32_t>(ws, L.knn_idx);
     a.knn_d2 = L.at<float>(ws, L.knn_d2);
     a.rev_cnt = L.at<int32_t>(ws, L.rev_cnt);

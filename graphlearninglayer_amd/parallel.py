@@ -30,3 +30,53 @@ def gather_predictions(U: torch.Tensor, group=None, async_op: bool = True):
     out = torch.empty((world * U.shape[0],) + tuple(U.shape[1:]), dtype=U.dtype, device=U.device)
     work = dist.all_gather_into_tensor(out, U, group=group, async_op=async_op)
     return out, work
+
+
+class PredictionGatherer:
+    """All-gather of per-rank predictions coalesced over `every` calls (at NS a
+    single gather moves 20 KB, so its ~10-30 us of launch and rendezvous latency, not bytes,
+    is the cost; one gather per `every` calls amortises it).
+
+    `add(U)` keeps a reference to this call's U (no copy, no collective); every `every`-th
+    call stacks the pending U's into one (every, m, C) tensor and issues ONE asynchronous
+    all_gather_into_tensor; `flush()` issues it for a partial group.  Completed groups land
+    in `self.gathered` as (world, every, m, C) tensors in call order once `wait()` returns.
+    With one rank (or no process group) it is a no-op that records nothing."""
+
+    def __init__(self, every: int = 8, group=None):
+        self.every = max(1, int(every))
+        self.group = group
+        self.pending = []
+        self.inflight = []      # (out tensor, work)
+        self.gathered = []
+
+    def _active(self) -> bool:
+        return (dist.is_available() and dist.is_initialized()
+                and dist.get_world_size(self.group) > 1)
+
+    def add(self, U: torch.Tensor) -> None:
+        if not self._active():
+            return
+        self.pending.append(U)
+        if len(self.pending) >= self.every:
+            self.flush()
+
+    def flush(self) -> None:
+        if not self.pending:
+            return
+        world = dist.get_world_size(self.group)
+        block = torch.stack([u.detach() for u in self.pending]).contiguous()
+        self.pending = []
+        # concatenated along dim 0 (the layout every backend accepts), viewed per rank below
+        out = torch.empty((world * block.shape[0],) + tuple(block.shape[1:]), dtype=block.dtype,
+                          device=block.device)
+        work = dist.all_gather_into_tensor(out, block, group=self.group, async_op=True)
+        self.inflight.append((out.view((world,) + tuple(block.shape)), work))
+
+    def wait(self) -> None:
+        """Flush the partial group and wait for every issued gather."""
+        self.flush()
+        for out, work in self.inflight:
+            work.wait()
+            self.gathered.append(out)
+        self.inflight = []

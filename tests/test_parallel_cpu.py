@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from graphlearninglayer_amd.parallel import gather_predictions, shard_rank_seed
+from graphlearninglayer_amd.parallel import PredictionGatherer, gather_predictions, shard_rank_seed
 from graphlearninglayer_amd.synth import CONFIGS, one_hot, synth
 from oracle import gll_oracle
 
@@ -72,3 +72,37 @@ def test_gather_predictions_single_process_is_identity():
 def test_shards_are_distinct_graphs():
     a, b = _shard_predictions(0), _shard_predictions(1)
     assert not torch.equal(a, b)
+
+
+def _coalesced_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = PredictionGatherer(every=3)
+        calls = [(_shard_predictions(rank) + s) for s in range(7)]   # 7 calls: groups 3, 3, 1
+        for U in calls:
+            g.add(U)
+        g.wait()
+        assert [t.shape for t in g.gathered] == [(world, 3, 64, 10), (world, 3, 64, 10),
+                                                 (world, 1, 64, 10)]
+        full = torch.cat([t.transpose(0, 1) for t in g.gathered])   # (calls, world, m, C)
+        np.save(os.path.join(out_dir, f"c{rank}.npy"), full.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_coalesced_gatherer_world2(tmp_path):
+    """bench.py's coalesced gather: every call's predictions of every rank, in call order."""
+    world = 2
+    mp.spawn(_coalesced_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    expect = np.stack([np.stack([(_shard_predictions(r) + s).numpy() for r in range(world)])
+                       for s in range(7)])
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"c{r}.npy"), expect)
+
+
+def test_coalesced_gatherer_single_process_is_noop():
+    g = PredictionGatherer(every=2)
+    g.add(torch.zeros(3, 2))
+    g.wait()
+    assert g.gathered == [] and g.pending == []
