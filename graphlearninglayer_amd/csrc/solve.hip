@@ -195,6 +195,11 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     float* P_ = smem + 128;                             // search direction (gathered)
     int* lcol = reinterpret_cast<int*>(P_ + ((m + 3) & ~3));   // overflow entries, compacted
     float* lw = reinterpret_cast<float*>(lcol + mat_cap);
+    // (Ordering rows by length so each wave's slot bound tracks its own rows was measured:
+    // no gain per iteration at NS, +1.5 us of setup from the permuted ELL loads.)
+    int urow[R];   // the row each thread slot handles
+#pragma unroll
+    for (int q = 0; q < R; ++q) urow[q] = tid + NT * q;
     int ec[R][S];
     float ew[R][S];
     int ost[R], olen[R];
@@ -214,7 +219,7 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     const bool has_ovf = __syncthreads_or(longer) != 0;
 #pragma unroll
     for (int q = 0; q < R; ++q) {
-        const int u = tid + NT * q;
+        const int u = urow[q];
         const int uc = u < m ? u : 0;
         x[q] = r[q] = p[q] = ap[q] = mi[q] = dg[q] = 0.f;
 #pragma unroll
@@ -276,7 +281,7 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
         int smax[R];
 #pragma unroll
         for (int q = 0; q < R; ++q) {
-            const int u = tid + NT * q;
+            const int u = urow[q];
             const int len = u < m ? ucnt[u] : 0;
             smax[q] = wave_max_int(len < S ? len : S);
         }
@@ -323,18 +328,29 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
         float gam = rz;
         float alpha = dl > 0.f ? gam / dl : 0.f;
         if (!(dl > 0.f)) alpha = -1.f;   // breakdown before the first step
+#ifdef GLL_TRACE
+#define GLL_TRACE_CYC(i)                                                                       \
+    do {                                                                                       \
+        if (it == 3 && blockIdx.x == 0 && threadIdx.x == 0) g_trace[i] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define GLL_TRACE_CYC(i) do {} while (0)
+#endif
         while (!conv && alpha > 0.f && it < max_iter) {
             ++it;
+            GLL_TRACE_CYC(10);
 #pragma unroll
             for (int q = 0; q < R; ++q) {
                 x[q] += alpha * p[q];
                 r[q] -= alpha * sv[q];
                 ap[q] = mi[q] * r[q];                       // u = M^-1 r
-                const int u = tid + NT * q;
+                const int u = urow[q];
                 if (u < m) P_[u] = ap[q];
             }
+            GLL_TRACE_CYC(11);
             if constexpr (NT > kWave) __syncthreads();
             if (it == 1) GLL_TRACE_PT(4);
+            GLL_TRACE_CYC(12);
             float gn = 0.f, de = 0.f, rr = 0.f;
             float w[R];
 #pragma unroll
@@ -344,22 +360,30 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
                 de += w[q] * ap[q];
                 rr += r[q] * r[q];
             }
+#ifdef GLL_TRACE
+            if (it == 3 && blockIdx.x == 0 && threadIdx.x == 0 && de == 12345.f) g_trace[9] = 0;
+#endif
+            GLL_TRACE_CYC(13);
             block_sum3<NT>(gn, de, rr, red, phase);
+            GLL_TRACE_CYC(14);
             if (it == 1) GLL_TRACE_PT(6);
             if (rr <= tol2) {
                 conv = true;
                 break;
             }
-            const float beta = gn / gam;
-            const float den = de - beta * gn / alpha;
+            // one reciprocal on the critical path: alpha' = gn / (de - beta gn / alpha)
+            //                                             = gn alpha / (alpha de - beta gn)
+            const float beta = gn * __builtin_amdgcn_rcpf(gam);
+            const float den = alpha * de - beta * gn;
             if (!(den > 0.f)) break;   // breakdown or NaN: reported as non-converged
-            alpha = gn / den;
+            alpha = (gn * alpha) * __builtin_amdgcn_rcpf(den);
             gam = gn;
 #pragma unroll
             for (int q = 0; q < R; ++q) {
                 p[q] = ap[q] + beta * p[q];
                 sv[q] = w[q] + beta * sv[q];
             }
+            GLL_TRACE_CYC(15);
         }
     } else {
     block_sum2<NT>(rz, bb, red, phase);
@@ -413,7 +437,7 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             p[q] = mi[q] * r[q] + beta * p[q];
-            const int u = tid + NT * q;
+            const int u = urow[q];
             if (u < m) P_[u] = p[q];
         }
         if constexpr (NT > kWave) __syncthreads();
@@ -423,7 +447,7 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     GLL_TRACE_PT(8);
 #pragma unroll
     for (int q = 0; q < R; ++q) {
-        const int u = tid + NT * q;
+        const int u = urow[q];
         if (u < m) {
             if (out64) out64[size_t(u) * C + c] = double(x[q]);
             if (out32) out32[size_t(u) * C + c] = x[q];

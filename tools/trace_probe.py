@@ -95,6 +95,12 @@ def timeline(tr, label):
         print("select wave 0: " + ", ".join(f"{nm} +{TICK_US * (g[q] - g[20]):.2f}" for q, nm in
                                            [(23, "row loaded"), (16, "scanned"), (17, "merged"), (18, "refined"),
                                             (19, "ranked+written")] if g[q]))
+    cyc = tr[2][10:16].astype(np.int64)
+    if cyc[0] and cyc[5]:
+        lab = ["update+store", "publish barrier", "spmv+dots", "reduce (dpp+lds+barrier)", "alpha/beta+p,s"]
+        print("cg block 0 wave 0, iteration 3 (shader cycles): " +
+              ", ".join(f"{lab[q]} {cyc[q + 1] - cyc[q]}" for q in range(5)) +
+              f" | total {cyc[5] - cyc[0]}")
     pts = tr[2][:10].astype(np.int64)
     if pts[0]:
         print("cg block 0: " + ", ".join(f"{CG_PTS[i]} +{TICK_US * (pts[i] - pts[0]):.2f}"
