@@ -29,7 +29,7 @@ constexpr int kStBump = 9;       //                        bump-region cursor
 // ELL slice width of the per-column CG kernels for m unlabeled rows (solve.hip dispatch);
 // row_build emits that many column-major (col, w) slots per U row, 0 when no ELL kernel runs.
 inline int ell_slots(int m) {
-    return m <= 512 ? 24 : (m <= 1024 ? 16 : (m <= 2048 ? 8 : (m <= 4096 ? 4 : 0)));
+    return m <= 512 ? 24 : (m <= 2048 ? 16 : (m <= 4096 ? 4 : 0));
 }
 
 // ---------------------------------------------------------------------------------------

@@ -301,15 +301,41 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
 #pragma unroll
             for (int s2 = 0; s2 < S; ++s2) acc += ew[q][s2] * pv[s2];
             if (matl) {
-                for (int t = 0; t < olen[q]; ++t) {
-                    const int e = ost[q] + t;
-                    acc += lw[e] * P_[lcol[e]];
+                // four entries per step, every LDS read issued before use (same summation
+                // order as one at a time); rows past the slots are long at K = 25
+                const int e0 = ost[q], no = olen[q];
+                int t = 0;
+                for (; t + 4 <= no; t += 4) {
+                    int c4[4];
+                    float w4[4], p4[4];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        c4[v] = lcol[e0 + t + v];
+                        w4[v] = lw[e0 + t + v];
+                    }
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) p4[v] = P_[c4[v]];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) acc += w4[v] * p4[v];
                 }
-            } else {
-                for (int t = 0; t < olen[q]; ++t) {
-                    const int e = ost[q] + t;
-                    acc += wv[e] * P_[col[e] - base];
+                for (; t < no; ++t) acc += lw[e0 + t] * P_[lcol[e0 + t]];
+            } else {   // from the CSR (L2), four entries in flight per step
+                const int e0 = ost[q], no = olen[q];
+                int t = 0;
+                for (; t + 4 <= no; t += 4) {
+                    int c4[4];
+                    float w4[4], p4[4];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        c4[v] = col[e0 + t + v];
+                        w4[v] = wv[e0 + t + v];
+                    }
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) p4[v] = P_[c4[v] - base];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) acc += w4[v] * p4[v];
                 }
+                for (; t < no; ++t) acc += wv[e0 + t] * P_[col[e0 + t] - base];
             }
             return dg[q] * pq - acc;   // (Luu u)_row = (deg + tau) u_row - sum_j W_rowj u_j
         };
@@ -400,15 +426,41 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
             for (int s = 0; s < S; ++s)
                 acc += ew[q][s] * P_[ec[q][s]];
             if (matl) {
-                for (int t = 0; t < olen[q]; ++t) {
-                    const int e = ost[q] + t;
-                    acc += lw[e] * P_[lcol[e]];
+                // four entries per step, every LDS read issued before use (same summation
+                // order as one at a time); rows past the slots are long at K = 25
+                const int e0 = ost[q], no = olen[q];
+                int t = 0;
+                for (; t + 4 <= no; t += 4) {
+                    int c4[4];
+                    float w4[4], p4[4];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        c4[v] = lcol[e0 + t + v];
+                        w4[v] = lw[e0 + t + v];
+                    }
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) p4[v] = P_[c4[v]];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) acc += w4[v] * p4[v];
                 }
-            } else {
-                for (int t = 0; t < olen[q]; ++t) {
-                    const int e = ost[q] + t;
-                    acc += wv[e] * P_[col[e] - base];
+                for (; t < no; ++t) acc += lw[e0 + t] * P_[lcol[e0 + t]];
+            } else {   // from the CSR (L2), four entries in flight per step
+                const int e0 = ost[q], no = olen[q];
+                int t = 0;
+                for (; t + 4 <= no; t += 4) {
+                    int c4[4];
+                    float w4[4], p4[4];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        c4[v] = col[e0 + t + v];
+                        w4[v] = wv[e0 + t + v];
+                    }
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) p4[v] = P_[c4[v] - base];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) acc += w4[v] * p4[v];
                 }
+                for (; t < no; ++t) acc += wv[e0 + t] * P_[col[e0 + t] - base];
             }
             ap[q] = dg[q] * p[q] - acc;   // (Luu p)_u = (deg_u + tau) p_u - sum_j W_uj p_j
             pap += p[q] * ap[q];
@@ -556,10 +608,11 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
                           double* out64, float* out32, float rtol, int max_iter,
                           int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
     size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4;
-    // entries past the ELL slices (rare: hub rows) are compacted into LDS up to kOvfLds of
-    // them, the rest read from the CSR; capped so 4 workgroups still share a CU in batched
-    // launches (a full-LDS request would pin one per CU)
-    constexpr int64_t kOvfLds = 2048;
+    // entries past the ELL slices are compacted into LDS up to kOvfLds of them, the rest read
+    // from the CSR; batched launches cap them so 4 workgroups still share a CU (a full-LDS
+    // request would pin one per CU); a single graph's C workgroups take all the LDS there is
+    // (K = 25 rows overflow 16 slots by ~14K entries at m = 1250)
+    const int64_t kOvfLds = bt.B == 1 ? int64_t(1) << 30 : 2048;
     const int64_t eu_bound = int64_t(L.m + L.n) * (L.K - 1);
     int64_t cap = int64_t(kLdsDyn - lds) / 8;
     if (cap > eu_bound) cap = eu_bound;
@@ -587,11 +640,12 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
                               int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
     const int m = L.m;
     // one persistent launch over the whole GPU (gridcg.hip) for a single graph past the
-    // per-column register kernels' sweet spot (m > 1024: their ELL slices overflow); measured
-    // at stress (m 4096, K 30): 209 us against 288 us per solve.  Batches keep the
+    // per-column register kernels' sweet spot (m > 2048: 4 ELL slots); measured at stress
+    // (m 4096, K 30): 209 us against 288 us per solve, while at the FullySup shape (m 1250,
+    // K 25) the per-column kernel with 16 slots and the LDS overflow wins.  Batches keep the
     // per-column kernels (B x C workgroups already fill the GPU).
     if (bt.B == 1 && L.C <= 16 && !(L.flags & GLL_FLAG_CG_PERCOL) &&
-        (m > 1024 || (L.flags & GLL_FLAG_CG_GRID))) {
+        (m > 2048 || (L.flags & GLL_FLAG_CG_GRID))) {
         const int b_dtype = sizeof(TB) == 8 ? GLL_DT_F64 : GLL_DT_F32;
         return launch_cg_grid_luu(L, ws, b, b_dtype, out64, out32, rtol, 0.f, max_iter,
                                   st_nonconv, st_iters, s);
@@ -613,7 +667,7 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     if (m <= 512 && bt.B == 1) GLL_ELL(512, 1, 24);
     if (m <= 512) GLL_ELL(256, 2, 24);
     if (m <= 1024) GLL_ELL(1024, 1, 16);
-    if (m <= 2048) GLL_ELL(1024, 2, 8);
+    if (m <= 2048) GLL_ELL(1024, 2, 16);
     if (m <= 4096) GLL_ELL(1024, 4, 4);
 #undef GLL_ELL
     const size_t vec_bytes = size_t(5) * m * sizeof(float);
