@@ -412,6 +412,18 @@ __global__ __launch_bounds__(768) void gram48_kernel(const float* __restrict__ X
 //     MFMAs into one 32 x 32 accumulator);
 //   - the 4 feature-quarter partials of each quadrant are summed in LDS in a fixed order.
 // --------------------------------------------------------------------------------------
+// XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs (block b runs on XCD
+// b % 8, MI355X_MICROARCH.md), so block b takes tile (b % 8) * ceil-share + b / 8: each XCD
+// works through a contiguous run of the row-major upper-triangle tile list -- a band of row
+// blocks bi whose rows stay in that XCD's L2 -- instead of every XCD touching every row.
+// (Measured neutral at NS, B = 64 and stress, tools/ab_flags.py: the tile loads are bound by
+// per-CU issue, not by L2 misses.)
+__device__ __forceinline__ int xcd_tile(int b, int nt) {
+    const int x = b & 7, q = b >> 3;
+    const int per = nt >> 3, extra = nt & 7;   // the first `extra` XCDs take one tile more
+    return x * per + (x < extra ? x : extra) + q;
+}
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int kBP = 256;            // features per phase
@@ -440,7 +452,7 @@ __global__ __launch_bounds__(1024) void gram_bf3_kernel(const float* __restrict_
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar row bases
     const int r = lane & 31, h = lane >> 5;
-    int bi = 0, rem = blockIdx.x;
+    int bi = 0, rem = xcd_tile(blockIdx.x, gridDim.x);
     while (rem >= T - bi) {
         rem -= T - bi;
         ++bi;
@@ -591,6 +603,170 @@ __global__ __launch_bounds__(1024) void gram_bf3_kernel(const float* __restrict_
         }
     }
     GLL_TRACE_PT(14);
+}
+
+// --------------------------------------------------------------------------------------
+// K1a (large problems and batches): split-bf16 Gram on 128 x 128 tiles.  With many tiles the
+// kernel is bound by the tile rows every CU pulls out of L2 (2 x 64 rows per 64-tile: 4.3 GB
+// at stress); a 128-tile halves those bytes per output.  16 waves, wave w owns the 32 x 32
+// sub-tile (w >> 2, w & 3) over the WHOLE feature range, so there is no cross-wave reduction.
+// Features go in phases of 128: thread t loads 4 features of row 32 s + (t >> 5) of the 256
+// tile rows (0..127 = rows bi*128.., 128..255 = rows bj*128..) for slot s = 0..7 -- half a
+// wave per 512-B row segment -- and splits them into hi / lo bf16 planes in LDS (row stride
+// 136 bf16: conflict-free ds_read_b128); one barrier, then 8 k-steps x 3 MFMAs per wave.
+// Off-diagonal tiles store straight from the accumulators in both orientations; diagonal
+// tiles go through LDS so D2 stays bitwise symmetric (upper triangle mirrored).
+// --------------------------------------------------------------------------------------
+constexpr int kWP = 128;            // features per phase
+constexpr int kWS = kWP + 8;        // LDS plane row stride (bf16)
+
+template <bool VEC>
+__global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict__ X, int n,
+                                                         int d, int T, float* __restrict__ D2,
+                                                         int ld, int32_t* __restrict__ status,
+                                                         int32_t* __restrict__ rev_cnt,
+                                                         size_t xs, size_t wss) {
+    X = gshift(X, xs);
+    D2 = gshift(D2, wss);
+    status = gshift(status, wss);
+    rev_cnt = gshift(rev_cnt, wss);
+    constexpr int kPlane = 256 * kWS;                                   // bf16 per plane
+    __shared__ __attribute__((aligned(16))) __bf16 smem_h[2 * kPlane];  // 136 KiB
+    __shared__ float nrm[256];
+    float* smem = reinterpret_cast<float*>(smem_h);
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    int bi = 0, rem = xcd_tile(blockIdx.x, gridDim.x);
+    while (rem >= T - bi) {
+        rem -= T - bi;
+        ++bi;
+    }
+    const int bj = bi + rem;
+    {   // per-call reset of the counters the select kernel accumulates into
+        const int g = blockIdx.x * 1024 + tid;
+        if (g < GLL_ST_NWORDS) status[g] = 0;
+        for (int q = g; q < n; q += gridDim.x * 1024) rev_cnt[q] = 0;
+    }
+    const int fo = 4 * (tid & 31);       // this thread's 4 features inside a phase
+    const int rs = tid >> 5;             // its row inside a slot (0..31)
+    auto slot_row = [&](int s) {         // tile row 32 s + rs; rows past n clamped
+        const int R = 32 * s + rs;
+        const int row = (R < 128 ? bi * 128 + R : bj * 128 + R - 128);
+        return X + size_t(row < n ? row : n - 1) * d;
+    };
+    const int nph = (d + kWP - 1) / kWP;
+    const int sa = w >> 2, sb = w & 3;   // this wave's 32 x 32 sub-tile
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    // row norms: slot q's half-wave sum is kept by lane q of that half-wave (one register)
+    float sq = 0.f;
+
+    auto gload = [&](int ph, f32x4 (&v)[8]) {
+        const int k = ph * kWP + fo;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = load4_raw<VEC>(slot_row(q), k, d);
+    };
+    auto phase = [&](int ph, const f32x4 (&v)[8]) {
+        const int k = ph * kWP + fo;
+        __syncthreads();   // the previous phase's fragment reads are done
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const f32x4 f = mask4<VEC>(v[q], k, d);
+            float t = f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+            t = dpp_add<0xB1, 0xf>(t);    // quad
+            t = dpp_add<0x4E, 0xf>(t);
+            t = dpp_add<0x141, 0xf>(t);   // half row (8)
+            t = dpp_add<0x140, 0xf>(t);   // row (16)
+            t += __shfl_xor(t, 16);       // the 32 lanes of the row segment
+            sq += (lane & 31) == q ? t : 0.f;
+            bf16x4 hv, lv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const __bf16 hb = static_cast<__bf16>(f[e]);
+                hv[e] = hb;
+                lv[e] = static_cast<__bf16>(f[e] - static_cast<float>(hb));
+            }
+            const int o = (32 * q + rs) * kWS + fo;
+            *reinterpret_cast<bf16x4*>(smem_h + o) = hv;
+            *reinterpret_cast<bf16x4*>(smem_h + kPlane + o) = lv;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int st = 0; st < kWP / 16; ++st) {
+            const int kk = 16 * st + 8 * h;
+            const int oa = (32 * sa + r) * kWS + kk, ob = (128 + 32 * sb + r) * kWS + kk;
+            const bf16x8 ha = *reinterpret_cast<const bf16x8*>(smem_h + oa);
+            const bf16x8 la = *reinterpret_cast<const bf16x8*>(smem_h + kPlane + oa);
+            const bf16x8 hb = *reinterpret_cast<const bf16x8*>(smem_h + ob);
+            const bf16x8 lb = *reinterpret_cast<const bf16x8*>(smem_h + kPlane + ob);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(la, hb, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha, lb, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha, hb, acc, 0, 0, 0);
+        }
+    };
+    {
+        f32x4 va[8], vb[8];
+        gload(0, va);
+        for (int ph = 0; ph < nph; ph += 2) {
+            gload(ph + 1 < nph ? ph + 1 : ph, vb);   // unconditional: static vmcnt counts
+            phase(ph, va);
+            if (ph + 1 >= nph) break;
+            gload(ph + 2 < nph ? ph + 2 : ph + 1, va);
+            phase(ph + 1, vb);
+        }
+    }
+    if ((lane & 31) < 8) nrm[32 * (lane & 31) + rs] = sq;   // tile row 32 q + rs, q = lane
+    __syncthreads();   // norms visible; fragment reads done (the planes may be reused)
+    // C layout of 32x32: col = lane & 31, row = (e&3) + 8(e>>2) + 4h
+    const int i0 = bi * 128 + 32 * sa, j0 = bj * 128 + 32 * sb;
+    float dv[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int rr = (e & 3) + 8 * (e >> 2) + 4 * h;
+        dv[e] = nrm[32 * sa + rr] + nrm[128 + 32 * sb + r] - 2.f * acc[e];
+    }
+    if (bi != bj) {
+        // direct orientation: element e is (i0 + rr, j0 + r) -- 32 lanes per 128-B row piece
+        const int j = j0 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int i = i0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            if (i < n && j < n) D2[size_t(i) * ld + j] = dv[e];
+        }
+        // mirrored: row j0 + r, columns i0 + 8 g + 4 h .. +3 are registers 4 g .. 4 g + 3
+        if (j < n) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int i = i0 + 8 * g + 4 * h;
+                float* dst = D2 + size_t(j) * ld + i;
+                if (i + 4 <= n) {
+                    *reinterpret_cast<f32x4*>(dst) =
+                        f32x4{dv[4 * g], dv[4 * g + 1], dv[4 * g + 2], dv[4 * g + 3]};
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        if (i + t < n) dst[t] = dv[4 * g + t];
+                }
+            }
+        }
+    } else {
+        // diagonal tile: stage [128][129] in LDS, store the upper triangle in both orientations
+        float* tile = smem;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int rr = 32 * sa + (e & 3) + 8 * (e >> 2) + 4 * h;
+            tile[rr * 129 + 32 * sb + r] = dv[e];
+        }
+        __syncthreads();
+        for (int q = tid; q < 128 * 128; q += 1024) {
+            const int ti = q >> 7, tj = q & 127;
+            const int i = bi * 128 + ti, j = bi * 128 + tj;
+            if (i < n && j < n) D2[size_t(i) * ld + j] = tj >= ti ? tile[ti * 129 + tj] : tile[tj * 129 + ti];
+        }
+    }
 }
 
 // --------------------------------------------------------------------------------------
@@ -881,6 +1057,56 @@ __device__ __forceinline__ bool merge_fast(uint64_t (&key)[KS], int kc, int seen
     return __ballot(popped == KS && seen > KS) != 0;
 }
 
+// Threshold merge: T = the kc-th smallest 32-bit key head (the D2 bits) over all lanes' lists,
+// by bisection -- each step is KS ballots and scalar popcounts, no DPP chain (~0.4 us against
+// ~2 us for kc arg-min rounds at NS).  Every list entry <= T is a candidate, ties at T
+// included, so the set is exact on the D2 values (at most 64).  Returns true when it may be
+// incomplete: some lane's whole list is <= T while that lane saw more columns, or more than 64
+// candidates tie in; the caller then re-runs the exact merge.
+template <int KS>
+__device__ __forceinline__ bool merge_threshold(const uint64_t (&key)[KS], int kc, int seen,
+                                                int* __restrict__ cand, int& ci, int& kce) {
+    const int lane = lane_id();
+    uint32_t hv[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) hv[s] = uint32_t(key[s] >> 32);   // empty slots: 0xFFFFFFFF
+    auto count_le = [&](uint32_t t) {
+        int c = 0;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) c += __popcll(__ballot(hv[s] <= t));
+        return c;
+    };
+    uint32_t lo = 0u, up = 0xFFFFFFFEu;
+    if (count_le(up) >= kc) {
+        while (lo < up) {   // smallest T with count_le(T) >= kc (wave-uniform, <= 32 steps)
+            const uint32_t mid = lo + ((up - lo) >> 1);
+            if (count_le(mid) >= kc) up = mid;
+            else lo = mid + 1u;
+        }
+    }
+    const uint32_t T = up;   // fewer than kc valid entries: all of them
+    const uint64_t below = (1ull << lane) - 1ull;
+    int mine = 0, before = 0, total = 0;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        const uint64_t mk = __ballot(hv[s] <= T);
+        mine += hv[s] <= T ? 1 : 0;
+        before += __popcll(mk & below);
+        total += __popcll(mk);
+    }
+    const bool redo = (__ballot(mine == KS && seen > KS) != 0) || total > kWave;
+    if (!redo) {   // a lane's entries <= T are a prefix of its sorted list
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            if (hv[s] <= T) cand[before + s] = int(uint32_t(key[s]));
+    }
+    __builtin_amdgcn_wave_barrier();   // a wave's LDS ops run in order: the reads see the stores
+    asm volatile("" ::: "memory");
+    kce = total;
+    ci = (!redo && lane < total) ? cand[lane] : -1;
+    return redo;
+}
+
 template <int KC, bool VEC, int NP, int PG>
 __global__ __launch_bounds__(256) void knn_select_kernel(
     const float* __restrict__ D2, int ld, size_t plane, const float* __restrict__ X, int n, int d, int K,
@@ -902,24 +1128,26 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     ovf = gshift(ovf, wss);
     status = gshift(status, wss);
     status_pub = gshift(status_pub, sts);
+    __shared__ int s_cand[4][kWave];
     const int lane = lane_id();
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;  // whole wave
 
-    // 1-2) candidates: short per-lane lists + fast merge, exact re-run when inexact
+    // 1-2) candidates: short per-lane lists + threshold merge, exact re-run when inexact
     const float* row = D2 + size_t(i) * ld;
     constexpr int KS = KC <= 16 ? 4 : 8;
-    int ci;
+    int ci, kce;
     {
         uint64_t key[KS];
         const int seen = scan_row<KS, NP>(row, plane, n, ld, i, key);
         GLL_TRACE_PT(16);
-        const bool redo = merge_fast<KS>(key, kc, seen, ci);
+        const bool redo = merge_threshold<KS>(key, kc, seen, s_cand[threadIdx.x >> 6], ci, kce);
         GLL_TRACE_PT(17);
         if (redo) {
             uint64_t full[KC];
             scan_row<KC, NP>(row, plane, n, ld, i, full);
             ci = merge_exact<KC>(full, kc);
+            kce = kc;
         }
     }
     // 3) exact squared distances, 8 candidates per pass (8 lanes each, across d).  PG passes
@@ -929,13 +1157,13 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     const int grp = lane >> 3, sub = lane & 7;
     const float* xi = X + size_t(i) * d;
     float ce = __builtin_inff();
-    for (int p0 = 0; p0 < kc; p0 += 8 * PG) {
+    for (int p0 = 0; p0 < kce; p0 += 8 * PG) {
         const float* xj[PG];
 #pragma unroll
         for (int g2 = 0; g2 < PG; ++g2) {
             const int idx = p0 + 8 * g2 + grp;
-            const int j = __shfl(ci, idx < kc ? idx : 0);
-            const bool live = idx < kc && j >= 0;
+            const int j = __shfl(ci, idx < kce ? idx : 0);
+            const bool live = idx < kce && j >= 0;
             xj[g2] = X + size_t(live ? j : i) * d;
         }
         float part[PG];
@@ -978,13 +1206,13 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     // 4) rank the candidates by (exact d^2, index); keep the K-1 nearest
     const uint64_t myk = ci < 0 ? ~0ull : pack_key(ce, ci);
     int rank = 0;
-    for (int u = 0; u < kc; ++u) {
+    for (int u = 0; u < kce; ++u) {
         const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(myk), u);
         const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(myk >> 32), u);
         const uint64_t ku = (uint64_t(hi) << 32) | lo;
         rank += ku < myk ? 1 : 0;
     }
-    const bool keep = lane < kc && ci >= 0 && rank < K - 1;
+    const bool keep = lane < kce && ci >= 0 && rank < K - 1;
     int32_t* oi = knn_idx + size_t(i) * K;
     float* od = knn_d2 + size_t(i) * K;
     if (lane == 0) {
@@ -1045,6 +1273,22 @@ static bool use_gram48(const Layout& L, const Batch& bt) {
 
 hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
                        hipStream_t s) {
+    if (L.KS == 1 && !(L.flags & GLL_FLAG_GRAM_F32) && !(L.flags & GLL_FLAG_GRAM_NARROW)) {
+        const int T = (L.n + 127) / 128;
+        if (int64_t(bt.B) * T * (T + 1) / 2 >= 512) {   // enough 128-tiles to fill the chip twice
+            const dim3 grid(T * (T + 1) / 2, bt.B);
+            float* D2 = L.at<float>(ws, L.D2);
+            int32_t* st = L.at<int32_t>(ws, L.status);
+            int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
+            prof_begin(GLL_K_GRAM, s);
+            if (vec)
+                gram_bf3w_kernel<true><<<grid, 1024, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
+            else
+                gram_bf3w_kernel<false><<<grid, 1024, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
+            prof_end(GLL_K_GRAM, s);
+            return launch_status("knn.hip:launch_gram(bf3w)");
+        }
+    }
     if (L.KS == 1 && !(L.flags & GLL_FLAG_GRAM_F32)) {
         const int T = (L.n + 63) / 64;
         const dim3 grid(T * (T + 1) / 2, bt.B);
