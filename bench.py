@@ -33,6 +33,11 @@ from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth  #
 METRIC = "GLL fwd+bwd calls/sec (base=500,batch=500,d=512,k=10) at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 MFMA_F32_PEAK_TFS = 157.3    # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), spec
+MFMA_BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA, spec (~2.5 PF; 2:1-sparse figures never used)
+# The Gram runs split-bf16 (x = hi + lo, three bf16 products per fp32 product) over the upper
+# triangle of tiles: ~1.5 executed bf16 MFMA flops per algorithmic flop 2n^2 d, so its MFMA
+# roof in algorithmic flops is the bf16 peak / 1.5.
+GRAM_ROOF_TFS = MFMA_BF16_PEAK_TFS / 1.5
 PROF_PERIOD = 8              # event-bracket every 8th launch of the dominant kernel
 GATHER_EVERY = 8             # calls per coalesced all_gather of the predictions
 EPS = {"plumbing": 1.0, "ns": 1.0, "fullysup": 1.0, "stress": "auto"}
@@ -73,9 +78,10 @@ def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps):
 
 
 # C-ABI kernel ids (gll_kernel_name) -> device symbols as rocprofv3 names them
-PMC_SYMBOLS = {"gram_d2_kernel": ["gram_bf3_kernel", "gram48_kernel", "gram_lds_kernel"], "knn_select_kernel": ["knn_select_kernel"],
+PMC_SYMBOLS = {"gram_d2_kernel": ["gram_bf3_kernel", "gram_bf3w_kernel", "gram48_kernel",
+                                   "gram_lds_kernel", "gram_wide_kernel"], "knn_select_kernel": ["knn_select_kernel"],
                "row_build_kernel": ["row_build_kernel"],
-               "cg_kernel": ["cg_ell_kernel", "cg_lds_kernel"],
+               "cg_kernel": ["cg_ell_kernel", "cg_grid_kernel", "cg_lds_kernel"],
                "edge_coef_kernel": ["edge_coef_kernel"], "grad_spmm_kernel": ["grad_spmm_kernel"]}
 
 
@@ -291,7 +297,7 @@ def main():
         bound, work = units[dominant]
         avg_s = ms / cnt / 1e3
         if bound == "mfma":
-            achieved, peak, unit = work / avg_s / 1e12, MFMA_F32_PEAK_TFS, "TFLOP/s"
+            achieved, peak, unit = work / avg_s / 1e12, GRAM_ROOF_TFS, "TFLOP/s"
         else:
             achieved, peak, unit = work / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
         roofline = {"kernel": dominant, "bound": bound, "achieved": round(achieved, 3),
@@ -299,11 +305,11 @@ def main():
                     "traffic": pmc_traffic(a.config, dominant), "work_per_launch": work,
                     "avg_launch_us": round(avg_s * 1e6, 3), "launches": cnt,
                     "cg_iters_fwd_bwd": list(iters)}
-        # whole-call roofline: kNN at the MFMA peak + every other byte at HBM
+        # whole-call roofline: kNN at its MFMA roof + every other byte at HBM
         f_knn = units["gram_d2_kernel"][1]
         b_rest = sum(w_ * per_kernel[kn]["launches_per_step"] for kn, (b_, w_) in units.items()
                      if b_ == "hbm" and kn in per_kernel)
-        call_roof_s = f_knn / (MFMA_F32_PEAK_TFS * 1e12) + b_rest / (HBM_PEAK_GBS * 1e9)
+        call_roof_s = f_knn / (GRAM_ROOF_TFS * 1e12) + b_rest / (HBM_PEAK_GBS * 1e9)
         for kn, v in per_kernel.items():
             b_, w_ = units[kn]
             v["algorithmic"] = (f"{w_ / 1e9:.4g} GFLOP" if b_ == "mfma" else f"{w_ / 1e6:.4g} MB")

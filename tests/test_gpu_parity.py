@@ -170,6 +170,28 @@ def test_hub_row_longer_than_lds_chunk():
     assert np.diff(rp).max() > 256
 
 
+def test_duplicate_points_and_ties():
+    """Clusters of exact duplicates: more tied candidates than the re-rank margin (the threshold
+    merge takes every tie at its threshold, more than 64 ties fall back to the exact merge), and
+    zero-distance pairs drop out of the graph as sparse.find drops them (GLL.py:198)."""
+    rng = np.random.default_rng(5)
+    n, d, base, k = 600, 40, 100, 10
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    X[200:230] = X[199]     # 31 copies: ties beyond K - 1 + margin
+    X[400:480] = X[399]     # 81 copies: more than 64 tied candidates
+    X[5:8] = X[4]           # duplicates among the labeled rows
+    lab = np.arange(n) % 10
+    Y = np.eye(10, dtype=np.float32)[lab[:base]]
+    gb = rng.standard_normal((n - base, 10))
+    U, grad = _run(X, Y, 0.07, 1.0, k, gb)
+    ind = _gpu_knn(X, k, 1.0)["knn_idx"].cpu().numpy()
+    assert O.knn_set_mismatch(X, ind, k) == []
+    Uo, st = O.forward(X, Y, 0.07, 1.0, k, knn=(ind, None))
+    assert O.rel_err(U, Uo) < TOL
+    assert O.rel_err(grad, O.backward(st, gb)) < TOL
+
+
 def test_no_labeled_rows_gives_zero_predictions():
     c = Case("plumbing_eps1p0_tau0p07_f32")
     GLL = _gll()
