@@ -21,6 +21,7 @@ GLL_TRACE_UNIT(rows)
 
 constexpr int kStage = 256;      // per-wave LDS staging capacity (entries)
 constexpr int kMaxCPerLane = 4;  // classes per lane in the rhs accumulation (C <= 256)
+constexpr int kYPre = 16;        // label prefetch: classes held per staged entry (C <= 16)
 
 struct RowArgs {
     int n, base, C, K, RCAP, Wcap;
@@ -87,12 +88,17 @@ __device__ __forceinline__ float yval(const TY* Y, int j, int C, int c) {
 
 // Build row i.  LDS: staging and sorted copies live in the wave's LDS slices; otherwise the
 // staging is tmp_col/tmp_d2 and the sorted copy is the output itself (agent fences order them).
-template <bool LDS, typename TY>
+// pri / prd: this lane's slot of the first 64 reverse entries, loaded with the kNN list (one
+// memory round trip for both).  Rows staged in LDS with C <= kYPre also issue the label loads
+// of their first 64 staged entries right after staging, so the loads overlap the sort and the
+// weights; the sums still run in sorted-column order (t_idx maps a sorted slot to its staged
+// entry), so results are unchanged.
+template <bool LDS, bool PRE, typename TY>
 __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict__ Y, int i,
                                           int start, int fi, float fd, bool fval,
-                                          uint64_t fmask, int nf, int rc, float ei,
-                                          int* s_col, float* s_d2, int* t_col, float* t_d2,
-                                          float* t_w) {
+                                          uint64_t fmask, int nf, int rc, float ei, int pri,
+                                          float prd, int* s_col, float* s_d2, int* t_col,
+                                          float* t_d2, float* t_w, int* t_idx, float* ybuf) {
     const int lane = lane_id();
     int* scol = LDS ? s_col : a.tmp_col + start;
     float* sd2 = LDS ? s_d2 : a.tmp_d2 + start;
@@ -113,8 +119,8 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
     for (int r0 = 0; r0 < nr; r0 += kWave) {
         const int r = r0 + lane;
         const bool live = r < nr;
-        const int ri = live ? a.rev_idx[size_t(i) * a.RCAP + r] : -1;
-        const float rd = live ? a.rev_d2[size_t(i) * a.RCAP + r] : 0.f;
+        const int ri = !live ? -1 : (r0 == 0 ? pri : a.rev_idx[size_t(i) * a.RCAP + r]);
+        const float rd = !live ? 0.f : (r0 == 0 ? prd : a.rev_d2[size_t(i) * a.RCAP + r]);
         bool dup = false;
         for (int t = 0; t < Km1; ++t) dup |= (ri == readlane_i(fself, t));
         const bool keep = live && !dup;
@@ -148,6 +154,15 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
         }
     }
     if constexpr (!LDS) __threadfence();
+    // label prefetch (unlabeled rows): lane e < 64 loads Y of staged entry e when labeled
+    const bool ypre = LDS && PRE && i >= a.base && a.C <= kYPre;
+    float yreg[kYPre];
+    if (ypre) {
+        const int col0 = lane < L ? scol[lane] : a.base;
+        const bool lab = lane < L && col0 < a.base;
+#pragma unroll
+        for (int c = 0; c < kYPre; ++c) yreg[c] = (lab && c < a.C) ? yval(Y, col0, a.C, c) : 0.f;
+    }
     // rank sort by column (columns are unique within a row)
     for (int e = lane; e < L; e += kWave) {
         const int c = scol[e];
@@ -155,6 +170,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
         for (int u = 0; u < L; ++u) rank += scol[u] < c ? 1 : 0;
         ocol[rank] = c;
         od2[rank] = sd2[e];
+        if constexpr (LDS && PRE) t_idx[rank] = e;
     }
     if constexpr (!LDS) __threadfence();
     // sorted pass: weights, degree, labeled-prefix length
@@ -192,7 +208,23 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
             a.ell_w[size_t(lane) * a.m + u] = we;
         }
     }
-    if (i >= a.base) {
+    if (ypre) {
+        // prefetched labels: staged entry e's row of Y at ybuf[e][.], summed in sorted order
+        if (lane < L && lane < kWave) {
+#pragma unroll
+            for (int c = 0; c < kYPre; ++c) ybuf[lane * kYPre + c] = yreg[c];
+        }
+        __builtin_amdgcn_wave_barrier();   // a wave's LDS ops run in order
+        asm volatile("" ::: "memory");
+        for (int e0 = 0; e0 < nlab; ++e0) {
+            const int e = t_idx[e0];
+            const float we = ow[e0];
+            const float yv = lane < a.C ? (e < kWave ? ybuf[e * kYPre + lane]
+                                                     : yval(Y, ocol[e0], a.C, lane))
+                                        : 0.f;
+            racc[0] += we * yv;
+        }
+    } else if (i >= a.base) {
         // 8 labeled neighbours per step, their label loads all in flight before any is used
         for (int e0 = 0; e0 < nlab; e0 += 8) {
             float we[8], yv[8][kMaxCPerLane];
@@ -236,7 +268,9 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
     }
 }
 
-template <typename TY>
+// PRE: label prefetch (single-graph launches; its 20 KiB of LDS halves the workgroups per CU
+// that batches need: B = 64 NS 72 -> 90 us with it)
+template <typename TY, bool PRE>
 __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __restrict__ Y,
                                                         size_t ys) {
     GLL_TRACE_SCOPE(0);
@@ -247,6 +281,8 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
     __shared__ int t_col[4][kStage];
     __shared__ float t_d2[4][kStage];
     __shared__ float t_w[4][kStage];
+    __shared__ int t_idx[4][PRE ? kStage : 1];
+    __shared__ float ybuf[4][PRE ? kWave * kYPre : 1];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
     const int i = blockIdx.x * 4 + wv;
@@ -263,6 +299,12 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
     const int nf = __popcll(fmask);
     const int rc = a.rev_cnt[i];
     const float ei = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[i];   // issued with the lists
+    int pri = -1;   // the first 64 reverse-list slots, speculatively with the kNN list
+    float prd = 0.f;
+    if (lane < a.RCAP) {
+        pri = a.rev_idx[size_t(i) * a.RCAP + lane];
+        prd = a.rev_d2[size_t(i) * a.RCAP + lane];
+    }
     const int lbound = nf + rc;
     int start = i * a.Wcap;
     if (lbound > a.Wcap) {
@@ -271,11 +313,11 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
         start = readlane_i(s0, 0);
     }
     if (lbound <= kStage)
-        build_row<true, TY>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, ei, s_col[wv],
-                            s_d2[wv], t_col[wv], t_d2[wv], t_w[wv]);
+        build_row<true, PRE, TY>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, ei, pri, prd, s_col[wv],
+                            s_d2[wv], t_col[wv], t_d2[wv], t_w[wv], t_idx[wv], ybuf[wv]);
     else
-        build_row<false, TY>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, ei, nullptr, nullptr,
-                             nullptr, nullptr, nullptr);
+        build_row<false, PRE, TY>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, ei, pri, prd, nullptr,
+                             nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
 }
 
 hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,
@@ -319,10 +361,18 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     a.wss = bt.ws;
     dim3 grid((L.n + 3) / 4, bt.B);
     prof_begin(GLL_K_FINALIZE, s);
-    if (y_dtype == GLL_DT_F32) row_build_kernel<float><<<grid, 256, 0, s>>>(a, static_cast<const float*>(Y), bt.y);
-    else if (y_dtype == GLL_DT_F64) row_build_kernel<double><<<grid, 256, 0, s>>>(a, static_cast<const double*>(Y), bt.y);
-    else if (y_dtype == GLL_DT_I64) row_build_kernel<int64_t><<<grid, 256, 0, s>>>(a, static_cast<const int64_t*>(Y), bt.y);
+#define GLL_ROWS(T)                                                                          \
+    do {                                                                                     \
+        if (bt.B == 1)                                                                       \
+            row_build_kernel<T, true><<<grid, 256, 0, s>>>(a, static_cast<const T*>(Y), bt.y);  \
+        else                                                                                 \
+            row_build_kernel<T, false><<<grid, 256, 0, s>>>(a, static_cast<const T*>(Y), bt.y); \
+    } while (0)
+    if (y_dtype == GLL_DT_F32) GLL_ROWS(float);
+    else if (y_dtype == GLL_DT_F64) GLL_ROWS(double);
+    else if (y_dtype == GLL_DT_I64) GLL_ROWS(int64_t);
     else return hipErrorInvalidValue;
+#undef GLL_ROWS
     prof_end(GLL_K_FINALIZE, s);
     return launch_status("rows.hip:launch_finalize");
 }
