@@ -29,6 +29,11 @@ int dtype_code(at::Tensor& t) {
 }
 
 at::Tensor features(const at::Tensor& X, const c10::Device& dev) {
+    // the common case (fp32, contiguous, aligned, on the device) needs no new tensor: every
+    // dispatcher call here is host time on the step's critical path (~0.5 us each)
+    if (X.device() == dev && X.scalar_type() == at::kFloat && X.is_contiguous() &&
+        reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0)
+        return X;
     at::Tensor X32 = X.detach().to(dev, at::kFloat).contiguous();
     if (reinterpret_cast<uintptr_t>(X32.data_ptr()) % 16) X32 = X32.clone();  // 16-B vector path
     return X32;
@@ -68,12 +73,12 @@ class LaplaceLearningFn : public torch::autograd::Function<LaplaceLearningFn> {
             X.is_cuda() ? X.device() : c10::Device(c10::kCUDA, c10::hip::current_device());
         c10::DeviceGuard guard(dev);
         at::Tensor X32 = features(X, dev);
-        at::Tensor Yd = Y.detach().to(dev);
+        at::Tensor Yd = Y.device() == dev ? Y : Y.detach().to(dev);
         const int ycode = dtype_code(Yd);
         const int64_t n = X.size(-2), d = X.size(-1), base = Y.size(-2), C = Y.size(-1);
         if (batched && Y.dim() == 2) Yd = Yd.unsqueeze(0).expand({B, base, C});   // shared labels
         TORCH_CHECK(!batched || Yd.size(0) == B, "label_matrix batch ", Yd.size(0), " != ", B);
-        Yd = Yd.contiguous();
+        if (!Yd.is_contiguous()) Yd = Yd.contiguous();
         gll_problem p = make_problem(n, d, base, C, k, tau, eps, max_iter, rtol, sink);
         const size_t nb = gll_workspace_bytes(&p);
         TORCH_CHECK(nb > 0, "unsupported GLL problem n=", n, " d=", d, " base=", base,
@@ -87,14 +92,10 @@ class LaplaceLearningFn : public torch::autograd::Function<LaplaceLearningFn> {
                  "gll_forward");
         ctx->save_for_backward({X});
         ctx->saved_data["ws"] = ws;
-        ctx->saved_data["base"] = base;
-        ctx->saved_data["C"] = C;
-        ctx->saved_data["k"] = k;
-        ctx->saved_data["tau"] = tau;
-        ctx->saved_data["eps"] = eps;
-        ctx->saved_data["max_iter"] = max_iter;
-        ctx->saved_data["rtol"] = rtol;
-        ctx->saved_data["sink"] = sink;
+        // the scalars as one list (one map entry instead of eight; all exact in a double,
+        // the sink address included: 48-bit)
+        ctx->saved_data["p"] = std::vector<double>{double(base), double(C), double(k), tau, eps,
+                                                   double(max_iter), rtol, double(sink)};
         return X.is_cuda() ? U : U.cpu();
     }
 
@@ -104,15 +105,14 @@ class LaplaceLearningFn : public torch::autograd::Function<LaplaceLearningFn> {
         const c10::Device dev = ws.device();
         c10::DeviceGuard guard(dev);
         const int64_t B = X.dim() == 3 ? X.size(0) : 1;
-        gll_problem p = make_problem(
-            X.size(-2), X.size(-1), ctx->saved_data["base"].toInt(), ctx->saved_data["C"].toInt(),
-            ctx->saved_data["k"].toInt(), ctx->saved_data["tau"].toDouble(),
-            ctx->saved_data["eps"].toDouble(), ctx->saved_data["max_iter"].toInt(),
-            ctx->saved_data["rtol"].toDouble(), ctx->saved_data["sink"].toInt());
+        const auto sv = ctx->saved_data["p"].toDoubleVector();
+        gll_problem p = make_problem(X.size(-2), X.size(-1), int64_t(sv[0]), int64_t(sv[1]),
+                                     int64_t(sv[2]), sv[3], sv[4], int64_t(sv[5]), sv[6],
+                                     int64_t(sv[7]));
         at::Tensor X32 = features(X, dev);
-        at::Tensor g = grads[0].to(dev);
+        at::Tensor g = grads[0].device() == dev ? grads[0] : grads[0].to(dev);
         if (g.scalar_type() != at::kFloat && g.scalar_type() != at::kDouble) g = g.to(at::kDouble);
-        g = g.contiguous();
+        if (!g.is_contiguous()) g = g.contiguous();
         const int gcode = g.scalar_type() == at::kFloat ? GLL_DT_F32 : GLL_DT_F64;
         at::Tensor gradX = at::empty(X.sizes(), X32.options());
         hipStream_t s = c10::hip::getCurrentHIPStream(dev.index()).stream();
