@@ -38,7 +38,8 @@ MFMA_BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA, spec (~2.5 PF; 2:1-sparse figure
 # triangle of tiles: ~1.5 executed bf16 MFMA flops per algorithmic flop 2n^2 d, so its MFMA
 # roof in algorithmic flops is the bf16 peak / 1.5.
 GRAM_ROOF_TFS = MFMA_BF16_PEAK_TFS / 1.5
-PROF_PERIOD = 8              # event-bracket every 8th launch of the dominant kernel
+PROF_PERIOD = 7              # event-bracket every 7th launch of the dominant kernel (odd: the
+                             # CG runs twice per step, so both the forward and adjoint get sampled)
 GATHER_EVERY = 8             # calls per coalesced all_gather of the predictions
 EPS = {"plumbing": 1.0, "ns": 1.0, "fullysup": 1.0, "stress": "auto"}
 TAU = {"plumbing": 0.07, "ns": 0.07, "fullysup": 0.07, "stress": 0.07}

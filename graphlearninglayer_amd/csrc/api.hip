@@ -20,7 +20,6 @@ namespace gll {
 struct ProfState {
     int period[GLL_K_COUNT] = {};     // 0 = off, p = bracket every p-th launch
     long count[GLL_K_COUNT] = {};
-    bool armed[GLL_K_COUNT] = {};
     bool on[GLL_K_COUNT] = {};
     std::vector<hipEvent_t> pending[GLL_K_COUNT];  // start, stop, start, stop, ...
     std::vector<hipEvent_t> pool;
@@ -38,31 +37,37 @@ struct ProfState {
 };
 static ProfState g_prof;
 
-void prof_begin(int kid, hipStream_t s) {
-    if (!g_prof.on[kid]) return;
-    std::lock_guard<std::mutex> lk(g_prof.mu);
-    g_prof.armed[kid] = (g_prof.count[kid]++ % g_prof.period[kid]) == 0;
-    if (!g_prof.armed[kid]) return;
-    hipEvent_t e = g_prof.get();
-    if (!e) return;
-    (void)hipEventRecord(e, s);
-    g_prof.pending[kid].push_back(e);
-}
+thread_local ArmedLaunch g_armed;
 
-void prof_end(int kid, hipStream_t s) {
+// prof_begin arms a (start, stop) pair for the next launch_k on this thread; the dispatch
+// packet records both, so the pair brackets exactly the first kernel of the region.
+void prof_begin(int kid, hipStream_t) {
     if (!g_prof.on[kid]) return;
     std::lock_guard<std::mutex> lk(g_prof.mu);
-    if (!g_prof.armed[kid]) return;
-    g_prof.armed[kid] = false;
-    if (g_prof.pending[kid].size() % 2 == 0) return;  // begin was not recorded
-    hipEvent_t e = g_prof.get();
-    if (!e) {
-        g_prof.pool.push_back(g_prof.pending[kid].back());
-        g_prof.pending[kid].pop_back();
+    if ((g_prof.count[kid]++ % g_prof.period[kid]) != 0) return;
+    hipEvent_t e0 = g_prof.get();
+    hipEvent_t e1 = e0 ? g_prof.get() : nullptr;
+    if (!e1) {
+        if (e0) g_prof.pool.push_back(e0);
         return;
     }
-    (void)hipEventRecord(e, s);
-    g_prof.pending[kid].push_back(e);
+    g_prof.pending[kid].push_back(e0);
+    g_prof.pending[kid].push_back(e1);
+    g_armed = ArmedLaunch{kid, e0, e1};
+}
+
+// A pair still armed at the end of the region was never consumed by a launch: drop it.
+void prof_end(int kid, hipStream_t) {
+    if (g_armed.kid != kid) return;
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    auto& v = g_prof.pending[kid];
+    if (v.size() >= 2 && v.back() == g_armed.e1) {
+        for (int i = 0; i < 2; ++i) {
+            g_prof.pool.push_back(v.back());
+            v.pop_back();
+        }
+    }
+    g_armed = ArmedLaunch{};
 }
 
 hipError_t launch_status(const char* what) {
@@ -265,7 +270,7 @@ int gll_prof_enable(int kid, int period) {
     g_prof.on[kid] = period > 0;
     g_prof.period[kid] = period > 0 ? period : 1;
     g_prof.count[kid] = 0;
-    g_prof.armed[kid] = false;
+    if (g_armed.kid == kid) g_armed = ArmedLaunch{};
     return GLL_OK;
 }
 

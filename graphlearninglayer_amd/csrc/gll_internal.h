@@ -3,6 +3,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -348,6 +349,27 @@ __device__ __forceinline__ T* gshift(T* p, size_t stride) {
 
 // Launch-error report (GLL_DEBUG=1 in the environment): which launcher failed and why.
 hipError_t launch_status(const char* what);
+
+// Every kernel goes out through launch_k.  When prof_begin has armed an event pair for the next
+// launch (gll_prof_enable: bench.py times its dominant kernel inside the timed region), the
+// events ride in the dispatch packet itself (hipExtLaunchKernelGGL start / stop), so they time
+// the kernel the way rocprofv3 does rather than the queue between two separate event packets.
+struct ArmedLaunch {
+    int kid = -1;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+extern thread_local ArmedLaunch g_armed;
+
+template <typename F, typename... Args>
+inline void launch_k(F fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, Args... args) {
+    if (g_armed.kid >= 0) {
+        const hipEvent_t e0 = g_armed.e0, e1 = g_armed.e1;
+        g_armed.kid = -1;
+        hipExtLaunchKernelGGL(fn, grid, block, uint32_t(lds), s, e0, e1, 0u, args...);
+    } else {
+        fn<<<grid, block, lds, s>>>(args...);
+    }
+}
 
 // ---------------------------------------------------------------------------------------
 // Launchers (host side, one per translation unit)

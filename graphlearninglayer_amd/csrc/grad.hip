@@ -179,9 +179,9 @@ static hipError_t grad_nd(const EdgeArgs& a, const Batch& bt, const float* X, fl
 #define GLL_GRAD(ND)                                                                        \
     do {                                                                                    \
         if (bt.B == 1 && ND <= 4)                                                           \
-            grad_spmm_kernel<AUTO, ND, VEC, true><<<grid, 256, 0, s>>>(a, X, out, bt.x, bt.gx);  \
+            launch_k(grad_spmm_kernel<AUTO, ND, VEC, true>, grid, 256, 0, s, a, X, out, bt.x, bt.gx);  \
         else                                                                                \
-            grad_spmm_kernel<AUTO, ND, VEC, false><<<grid, 256, 0, s>>>(a, X, out, bt.x, bt.gx); \
+            launch_k(grad_spmm_kernel<AUTO, ND, VEC, false>, grid, 256, 0, s, a, X, out, bt.x, bt.gx); \
     } while (0)
     if (nd <= 1) GLL_GRAD(1);
     else if (nd <= 2) GLL_GRAD(2);
@@ -218,7 +218,7 @@ hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, cons
     hipError_t e;
     if (auto_eps) {
         prof_begin(GLL_K_EDGE, s);
-        edge_coef_kernel<<<dim3((L.n + 3) / 4, bt.B), 256, 0, s>>>(a);
+        launch_k(edge_coef_kernel, dim3((L.n + 3) / 4, bt.B), 256, 0, s, a);
         prof_end(GLL_K_EDGE, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         prof_begin(GLL_K_GRAD, s);

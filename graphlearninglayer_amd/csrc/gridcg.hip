@@ -428,7 +428,7 @@ static hipError_t launch_grid(const Mat& A, GridCgArgs a, int G, float* ws, hipS
     a.part = a.Zbuf + size_t(a.m) * a.Cp;
     hipError_t e = hipMemsetAsync(a.sync, 0, 16, s);
     if (e != hipSuccess) return e;
-    cg_grid_kernel<Mat, LPR, RPG><<<dim3(unsigned(G)), kGT, 0, s>>>(A, a);
+    launch_k(cg_grid_kernel<Mat, LPR, RPG>, dim3(unsigned(G)), kGT, 0, s, A, a);
     return launch_status("gridcg.hip:launch_grid");
 }
 

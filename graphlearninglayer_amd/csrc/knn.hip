@@ -1282,9 +1282,9 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
             int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
             prof_begin(GLL_K_GRAM, s);
             if (vec)
-                gram_bf3w_kernel<true><<<grid, 1024, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
+                launch_k(gram_bf3w_kernel<true>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
             else
-                gram_bf3w_kernel<false><<<grid, 1024, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
+                launch_k(gram_bf3w_kernel<false>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
             prof_end(GLL_K_GRAM, s);
             return launch_status("knn.hip:launch_gram(bf3w)");
         }
@@ -1297,9 +1297,9 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
         prof_begin(GLL_K_GRAM, s);
         if (vec)
-            gram_bf3_kernel<true><<<grid, 1024, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
+            launch_k(gram_bf3_kernel<true>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
         else
-            gram_bf3_kernel<false><<<grid, 1024, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
+            launch_k(gram_bf3_kernel<false>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
         prof_end(GLL_K_GRAM, s);
         return launch_status("knn.hip:launch_gram(bf3)");
     }
@@ -1312,7 +1312,7 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         const int nchunk = (L.d + kGK - 1) / kGK;
         prof_begin(GLL_K_GRAM, s);
 #define GLL_G48(V, N) \
-    gram48_kernel<V, N><<<grid, 768, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws)
+    launch_k(gram48_kernel<V, N>, grid, 768, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws)
         if (vec) { if (nchunk >= 4) GLL_G48(true, 4); else if (nchunk >= 2) GLL_G48(true, 2); else GLL_G48(true, 1); }
         else { if (nchunk >= 4) GLL_G48(false, 4); else if (nchunk >= 2) GLL_G48(false, 2); else GLL_G48(false, 1); }
 #undef GLL_G48
@@ -1328,7 +1328,7 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         const int nchunk = (L.d + kWK - 1) / kWK;
         prof_begin(GLL_K_GRAM, s);
 #define GLL_WIDE(V, N) \
-    gram_wide_kernel<V, N><<<grid, 256, 0, s>>>(X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws)
+    launch_k(gram_wide_kernel<V, N>, grid, 256, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws)
         if (vec) { if (nchunk >= 2) GLL_WIDE(true, 2); else GLL_WIDE(true, 1); }
         else { if (nchunk >= 2) GLL_WIDE(false, 2); else GLL_WIDE(false, 1); }
 #undef GLL_WIDE
@@ -1353,7 +1353,7 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
     const dim3 grid(tiles * KS, bt.B);
     prof_begin(GLL_K_GRAM, s);
 #define GLL_GRAM(V, N, G)                                                                         \
-    gram_lds_kernel<V, N, G><<<grid, 512, 0, s>>>(X, L.n, L.d, T, KS, kspan, D2, L.ldD, plane, st, \
+    launch_k(gram_lds_kernel<V, N, G>, grid, 512, 0, s, X, L.n, L.d, T, KS, kspan, D2, L.ldD, plane, st, \
                                                    rc, bt.x, bt.ws)
     if (vec) {
         if (NCH == 2) GLL_GRAM(true, 2, GK); else GLL_GRAM(true, 1, GK);
@@ -1381,7 +1381,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     prof_begin(GLL_K_SELECT, s);
     const size_t plane = size_t(n) * L.ldD;
 #define GLL_SEL3(KCV, V, NPV)                                                                  \
-    (bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2> : knn_select_kernel<KCV, V, NPV, 1>)<<<grid, 256, 0, s>>>( \
+    launch_k((bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2> : knn_select_kernel<KCV, V, NPV, 1>), grid, 256, 0, s,  \
         L.at<float>(ws, L.D2), L.ldD, plane, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0,     \
         L.RCAP,                                                                                \
         L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \

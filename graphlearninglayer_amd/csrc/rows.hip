@@ -364,9 +364,9 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
 #define GLL_ROWS(T)                                                                          \
     do {                                                                                     \
         if (bt.B == 1)                                                                       \
-            row_build_kernel<T, true><<<grid, 256, 0, s>>>(a, static_cast<const T*>(Y), bt.y);  \
+            launch_k(row_build_kernel<T, true>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y);  \
         else                                                                                 \
-            row_build_kernel<T, false><<<grid, 256, 0, s>>>(a, static_cast<const T*>(Y), bt.y); \
+            launch_k(row_build_kernel<T, false>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y); \
     } while (0)
     if (y_dtype == GLL_DT_F32) GLL_ROWS(float);
     else if (y_dtype == GLL_DT_F64) GLL_ROWS(double);

@@ -626,7 +626,7 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
     }
     auto fn = cg_ell_kernel<NT, R, S, TB, CGC>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
-    fn<<<dim3(L.C, bt.B), NT, lds, s>>>(
+    launch_k(fn, dim3(L.C, bt.B), NT, lds, s, 
         L.m, L.C, L.base, L.at<int32_t>(ws, L.row_start), L.at<int32_t>(ws, L.row_len),
         L.at<int32_t>(ws, L.ucnt), L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
         L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, int(cap), st_nonconv, st_iters,
@@ -675,7 +675,7 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     const size_t lds = 64 * 4 + (vec_lds ? vec_bytes : 0);
     auto fn = cg_lds_kernel<1024, TB>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
-    fn<<<dim3(L.C, bt.B), 1024, lds, s>>>(
+    launch_k(fn, dim3(L.C, bt.B), 1024, lds, s, 
         m, L.C, L.base, L.at<int32_t>(ws, L.row_start), L.at<int32_t>(ws, L.row_len),
         L.at<int32_t>(ws, L.ucnt), L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
         L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, L.at<float>(ws, L.cgv),
@@ -786,7 +786,7 @@ hipError_t launch_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* co
     auto fn = cg_csr_kernel<256>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
     prof_begin(GLL_K_CG, s);
-    fn<<<C, 256, lds, s>>>(m, C, row_ptr, col, val, b, x, atol, max_iter, gvec, vec_lds ? 1 : 0,
+    launch_k(fn, C, 256, lds, s, m, C, row_ptr, col, val, b, x, atol, max_iter, gvec, vec_lds ? 1 : 0,
                            iters, nonconv);
     prof_end(GLL_K_CG, s);
     return launch_status("solve.hip:launch_cg_csr");
