@@ -340,8 +340,20 @@ struct Batch {
     size_t st = 0;   // public status words: ws when they live in the workspace, 0 for a sink
 };
 
+// Branch-free on purpose: a branch per pointer splits the prologue into basic blocks with an
+// s_waitcnt each, serialising the kernel-argument loads (~13 dependent scalar loads, ~0.5 us
+// at the start of every kernel); selects let them all be in flight at once.
 template <typename T>
 __device__ __forceinline__ T* gshift(T* p, size_t stride) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uintptr_t off = uintptr_t(blockIdx.y) * stride;
+    return reinterpret_cast<T*>(a + (a != 0 ? off : uintptr_t(0)));
+}
+
+// Branching form for the register-tight Gram kernels (four pointers, no long load chain):
+// the select form costs them 36-84 B more of scratch spills.
+template <typename T>
+__device__ __forceinline__ T* gshift_br(T* p, size_t stride) {
     if (p == nullptr || stride == 0) return p;
     using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
     return reinterpret_cast<T*>(reinterpret_cast<B*>(p) + size_t(blockIdx.y) * stride);

@@ -70,10 +70,10 @@ __global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__
                                                        int32_t* __restrict__ rev_cnt,
                                                        size_t xs, size_t wss) {
     GLL_TRACE_SCOPE(0);
-    X = gshift(X, xs);
-    D2 = gshift(D2, wss);
-    status = gshift(status, wss);
-    rev_cnt = gshift(rev_cnt, wss);
+    X = gshift_br(X, xs);
+    D2 = gshift_br(D2, wss);
+    status = gshift_br(status, wss);
+    rev_cnt = gshift_br(rev_cnt, wss);
     constexpr int kGL = GK + 4;
     constexpr int CS = GK / 64;   // 64-column segments of a chunk row
     // stage[buf][A|B][64 rows][kGL]; the epilogue reuses the same storage
@@ -252,10 +252,10 @@ __global__ __launch_bounds__(768) void gram48_kernel(const float* __restrict__ X
                                                      int32_t* __restrict__ rev_cnt,
                                                      size_t xs, size_t wss) {
     GLL_TRACE_SCOPE(3);
-    X = gshift(X, xs);
-    D2 = gshift(D2, wss);
-    status = gshift(status, wss);
-    rev_cnt = gshift(rev_cnt, wss);
+    X = gshift_br(X, xs);
+    D2 = gshift_br(D2, wss);
+    status = gshift_br(status, wss);
+    rev_cnt = gshift_br(rev_cnt, wss);
     // stage[buf][A|B][48][k48L]; the epilogue reuses it: partials [4][3][3][4][64], norms
     // 2 x [4][3][64], tile [48][49] -- sized for the larger of the two
     constexpr int kStage = 2 * 2 * 48 * k48L;
@@ -437,10 +437,10 @@ __global__ __launch_bounds__(1024) void gram_bf3_kernel(const float* __restrict_
                                                         size_t xs, size_t wss) {
     GLL_TRACE_SCOPE(4);
     GLL_TRACE_PT(10);
-    X = gshift(X, xs);
-    D2 = gshift(D2, wss);
-    status = gshift(status, wss);
-    rev_cnt = gshift(rev_cnt, wss);
+    X = gshift_br(X, xs);
+    D2 = gshift_br(D2, wss);
+    status = gshift_br(status, wss);
+    rev_cnt = gshift_br(rev_cnt, wss);
     // hi plane [128][kBS] then lo plane [128][kBS] (bf16); after the k loop the space holds
     // the partial quadrants [kq][qd][32][33] and then the finished tile [64][65] (floats)
     constexpr int kPlane = 128 * kBS;                                   // bf16 per plane
@@ -626,10 +626,10 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
                                                          int ld, int32_t* __restrict__ status,
                                                          int32_t* __restrict__ rev_cnt,
                                                          size_t xs, size_t wss) {
-    X = gshift(X, xs);
-    D2 = gshift(D2, wss);
-    status = gshift(status, wss);
-    rev_cnt = gshift(rev_cnt, wss);
+    X = gshift_br(X, xs);
+    D2 = gshift_br(D2, wss);
+    status = gshift_br(status, wss);
+    rev_cnt = gshift_br(rev_cnt, wss);
     constexpr int kPlane = 256 * kWS;                                   // bf16 per plane
     __shared__ __attribute__((aligned(16))) __bf16 smem_h[2 * kPlane];  // 136 KiB
     __shared__ float nrm[256];
@@ -785,10 +785,10 @@ __global__ __launch_bounds__(256) void gram_wide_kernel(const float* __restrict_
                                                         int32_t* __restrict__ rev_cnt,
                                                         size_t xs, size_t wss) {
     GLL_TRACE_SCOPE(2);
-    X = gshift(X, xs);
-    D2 = gshift(D2, wss);
-    status = gshift(status, wss);
-    rev_cnt = gshift(rev_cnt, wss);
+    X = gshift_br(X, xs);
+    D2 = gshift_br(D2, wss);
+    status = gshift_br(status, wss);
+    rev_cnt = gshift_br(rev_cnt, wss);
     // stage[buf][A|B][128][kWL]; the epilogue reuses it as tile[128][129]
     __shared__ __attribute__((aligned(16))) float smem[2 * 2 * 128 * kWL];
     __shared__ float s_sq[2][128];

@@ -77,8 +77,12 @@ __device__ __forceinline__ void block_sum2(float& a, float& b, float* red, int& 
 
 // Block-wide sum of three values in one LDS exchange (the single-reduction CG).  Partials
 // are laid out [value][wave] so each total is read with 16-B loads; fixed order everywhere.
+// Block-wide sum of three values in two halves: post (DPP, partials to LDS, barrier) and read
+// (totals from LDS), so the pipelined CG can put independent work between them.  Partials
+// are laid out [value][wave] so each total is read with 16-B loads; fixed order everywhere.
 template <int NT>
-__device__ __forceinline__ void block_sum3(float& a, float& b, float& c, float* red, int& phase) {
+__device__ __forceinline__ const float* block_sum3_post(float& a, float& b, float& c, float* red,
+                                                        int& phase) {
     a = dpp_add<0xB1, 0xf>(a); b = dpp_add<0xB1, 0xf>(b); c = dpp_add<0xB1, 0xf>(c);
     a = dpp_add<0x4E, 0xf>(a); b = dpp_add<0x4E, 0xf>(b); c = dpp_add<0x4E, 0xf>(c);
     a = dpp_add<0x141, 0xf>(a); b = dpp_add<0x141, 0xf>(b); c = dpp_add<0x141, 0xf>(c);
@@ -89,9 +93,10 @@ __device__ __forceinline__ void block_sum3(float& a, float& b, float& c, float* 
         a = readlane_f(a, 63);
         b = readlane_f(b, 63);
         c = readlane_f(c, 63);
+        return red;
     } else {
         constexpr int NW = NT / kWave;
-        constexpr int NQ = NW < 4 ? 4 : NW;          // 16-B rows
+        constexpr int NQ = NW < 4 ? 4 : NW;
         float* q = red + phase * 3 * NQ;
         phase ^= 1;
         if (lane_id() == 63) {
@@ -101,6 +106,15 @@ __device__ __forceinline__ void block_sum3(float& a, float& b, float& c, float* 
             q[2 * NQ + w] = c;
         }
         __syncthreads();
+        return q;
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ void block_sum3_read(const float* q, float& a, float& b, float& c) {
+    if constexpr (NT > kWave) {
+        constexpr int NW = NT / kWave;
+        constexpr int NQ = NW < 4 ? 4 : NW;
         a = b = c = 0.f;
         if constexpr (NW % 4 == 0) {
 #pragma unroll
@@ -121,6 +135,14 @@ __device__ __forceinline__ void block_sum3(float& a, float& b, float& c, float* 
             }
         }
     }
+}
+
+// Block-wide sum of three values in one LDS exchange (the single-reduction CG).  Partials
+// are laid out [value][wave] so each total is read with 16-B loads; fixed order everywhere.
+template <int NT>
+__device__ __forceinline__ void block_sum3(float& a, float& b, float& c, float* red, int& phase) {
+    const float* q = block_sum3_post<NT>(a, b, c, red, phase);
+    block_sum3_read<NT>(q, a, b, c);
 }
 
 // Wave-uniform maximum of a small non-negative int (setup only).
@@ -164,7 +186,9 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int& total) 
     }
 }
 
-template <int NT, int R, int S, typename TB, bool CGC>
+// MODE: 0 classic PCG (two reductions), 1 Chronopoulos-Gear (one reduction, two barriers),
+// 2 pipelined PCG (Ghysels-Vanroose: one barrier per iteration).
+template <int NT, int R, int S, typename TB, int MODE>
 __global__ __launch_bounds__(NT) void cg_ell_kernel(
     int m, int C, int base, const int32_t* __restrict__ row_start,
     const int32_t* __restrict__ row_len, const int32_t* __restrict__ ucnt,
@@ -177,23 +201,24 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     extern __shared__ __attribute__((aligned(16))) float smem[];
     ell_col = gshift(ell_col, wss);
     ell_w = gshift(ell_w, wss);
-    row_start = gshift(row_start, wss);   // batched launches: graph blockIdx.y
-    row_len = gshift(row_len, wss);
+    row_start = gshift_br(row_start, wss);   // batched launches: graph blockIdx.y
+    row_len = gshift_br(row_len, wss);
     ucnt = gshift(ucnt, wss);
-    col = gshift(col, wss);
-    wv = gshift(wv, wss);
+    col = gshift_br(col, wss);
+    wv = gshift_br(wv, wss);
     diag = gshift(diag, wss);
     bsrc = gshift(bsrc, bs);
-    out64 = gshift(out64, us);
-    out32 = gshift(out32, wss);
-    st_nonconv = gshift(st_nonconv, sts);
-    st_iters = gshift(st_iters, sts);
+    out64 = gshift_br(out64, us);
+    out32 = gshift_br(out32, wss);
+    st_nonconv = gshift_br(st_nonconv, sts);
+    st_iters = gshift_br(st_iters, sts);
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
     float* red = smem;                                  // 96 floats of reduction scratch
     int* scan = reinterpret_cast<int*>(smem + 96);      // 16 ints of scan scratch
-    float* P_ = smem + 128;                             // search direction (gathered)
-    int* lcol = reinterpret_cast<int*>(P_ + ((m + 3) & ~3));   // overflow entries, compacted
+    const int mp4 = (m + 3) & ~3;
+    float* P_ = smem + 128;                             // gathered vector (x2 when pipelined)
+    int* lcol = reinterpret_cast<int*>(P_ + (MODE == 2 ? 2 : 1) * mp4);   // overflow, compacted
     float* lw = reinterpret_cast<float*>(lcol + mat_cap);
     // (Ordering rows by length so each wave's slot bound tracks its own rows was measured:
     // no gain per iteration at NS, +1.5 us of setup from the permuted ELL loads.)
@@ -208,40 +233,56 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     int tov = 0;
     GLL_TRACE_SCOPE(0);
     GLL_TRACE_PT(0);
+    // Every global load of the setup is issued before the first barrier (the U-block lengths,
+    // the ELL slices, the diagonal and the right-hand side), so the prologue pays one memory
+    // latency, not one per dependent step.
+    int ulen[R];
+    float bv[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int u = urow[q];
+        const int uc = u < m ? u : 0;
+        ulen[q] = ucnt[uc];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {   // column-major ELL slices (row_build): coalesced, padded
+            ec[q][s] = ell_col[size_t(s) * m + uc];
+            ew[q][s] = ell_w[size_t(s) * m + uc];
+        }
+        dg[q] = diag[uc];
+        bv[q] = to_f32(bsrc[size_t(uc) * C + c]);
+    }
     // entries past the S ELL slots exist only when some U block is longer than S: one
     // workgroup-wide OR (a single barrier) decides, so the usual case skips the overflow scan
     int longer = 0;
 #pragma unroll
     for (int q = 0; q < R; ++q) {
-        const int u = tid + NT * q;
-        longer |= (u < m && ucnt[u] > S) ? 1 : 0;
+        if (urow[q] >= m) ulen[q] = 0;
+        longer |= ulen[q] > S ? 1 : 0;
     }
     const bool has_ovf = __syncthreads_or(longer) != 0;
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int u = urow[q];
-        const int uc = u < m ? u : 0;
-        x[q] = r[q] = p[q] = ap[q] = mi[q] = dg[q] = 0.f;
+        x[q] = r[q] = p[q] = ap[q] = mi[q] = 0.f;
+        if (u >= m) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) {   // column-major ELL slices (row_build): coalesced, padded
-            const int cc = ell_col[size_t(s) * m + uc];
-            const float ww = ell_w[size_t(s) * m + uc];
-            ec[q][s] = u < m ? cc : 0;
-            ew[q][s] = u < m ? ww : 0.f;
+            for (int s = 0; s < S; ++s) {
+                ec[q][s] = 0;
+                ew[q][s] = 0.f;
+            }
+            dg[q] = 0.f;
         }
         ost[q] = 0;
         olen[q] = 0;
         if (has_ovf && u < m) {
-            const int len = ucnt[u];   // U block = sorted suffix of graph row base + u
+            const int len = ulen[q];   // U block = sorted suffix of graph row base + u
             ost[q] = row_start[base + u] + row_len[base + u] - len + S;
             olen[q] = len - S;
             tov += olen[q] > 0 ? olen[q] : 0;
         }
         if (u < m) {
-            dg[q] = diag[u];
             mi[q] = dg[q] > 0.f ? 1.f / dg[q] : 0.f;
-            const float bu = to_f32(bsrc[size_t(u) * C + c]);
-            r[q] = mi[q] > 0.f ? bu : 0.f;   // zero-diagonal rows are decoupled: x = 0
+            r[q] = mi[q] > 0.f ? bv[q] : 0.f;   // zero-diagonal rows are decoupled: x = 0
             p[q] = mi[q] * r[q];
             P_[u] = p[q];
             rz += r[q] * p[q];
@@ -272,26 +313,19 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     if constexpr (NT > kWave) __syncthreads();
     int it = 0;
     bool conv;
-    if constexpr (CGC) {
-        // Chronopoulos-Gear single-reduction PCG: one fused (r.u, w.u, r.r) exchange and one
-        // publish barrier per iteration (classic PCG: two exchanges + publish = 3 barriers).
-        // s = A p by recurrence; u = M^-1 r is what is published and multiplied.
+    if constexpr (MODE != 0) {
         // Each wave gathers only the ELL slots some row of its own holds (wave-uniform bound
         // in groups of 4: rows average ~6 of the 24 slots at NS).
         int smax[R];
 #pragma unroll
-        for (int q = 0; q < R; ++q) {
-            const int u = urow[q];
-            const int len = u < m ? ucnt[u] : 0;
-            smax[q] = wave_max_int(len < S ? len : S);
-        }
-        auto spmv = [&](int q, float pq) {
+        for (int q = 0; q < R; ++q) smax[q] = wave_max_int(ulen[q] < S ? ulen[q] : S);
+        auto spmv = [&](int q, float pq, const float* Pb) {
             float pv[S];
 #pragma unroll
             for (int s0 = 0; s0 < S; s0 += 4) {
                 if (s0 < smax[q]) {
 #pragma unroll
-                    for (int t = 0; t < 4 && s0 + t < S; ++t) pv[s0 + t] = P_[ec[q][s0 + t]];
+                    for (int t = 0; t < 4 && s0 + t < S; ++t) pv[s0 + t] = Pb[ec[q][s0 + t]];
                 } else {
 #pragma unroll
                     for (int t = 0; t < 4 && s0 + t < S; ++t) pv[s0 + t] = 0.f;
@@ -314,11 +348,11 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
                         w4[v] = lw[e0 + t + v];
                     }
 #pragma unroll
-                    for (int v = 0; v < 4; ++v) p4[v] = P_[c4[v]];
+                    for (int v = 0; v < 4; ++v) p4[v] = Pb[c4[v]];
 #pragma unroll
                     for (int v = 0; v < 4; ++v) acc += w4[v] * p4[v];
                 }
-                for (; t < no; ++t) acc += lw[e0 + t] * P_[lcol[e0 + t]];
+                for (; t < no; ++t) acc += lw[e0 + t] * Pb[lcol[e0 + t]];
             } else {   // from the CSR (L2), four entries in flight per step
                 const int e0 = ost[q], no = olen[q];
                 int t = 0;
@@ -331,20 +365,24 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
                         w4[v] = wv[e0 + t + v];
                     }
 #pragma unroll
-                    for (int v = 0; v < 4; ++v) p4[v] = P_[c4[v] - base];
+                    for (int v = 0; v < 4; ++v) p4[v] = Pb[c4[v] - base];
 #pragma unroll
                     for (int v = 0; v < 4; ++v) acc += w4[v] * p4[v];
                 }
-                for (; t < no; ++t) acc += wv[e0 + t] * P_[col[e0 + t] - base];
+                for (; t < no; ++t) acc += wv[e0 + t] * Pb[col[e0 + t] - base];
             }
             return dg[q] * pq - acc;   // (Luu u)_row = (deg + tau) u_row - sum_j W_rowj u_j
         };
+        if constexpr (MODE == 1) {
+        // Chronopoulos-Gear single-reduction PCG: one fused (r.u, w.u, r.r) exchange and one
+        // publish barrier per iteration (classic PCG: two exchanges + publish = 3 barriers).
+        // s = A p by recurrence; u = M^-1 r is what is published and multiplied.
         // pre-step: w0 = A u0 (u0 = p, already published), gamma0 = (r,u), delta0 = (w,u)
         float sv[R];
         float dl = 0.f;
 #pragma unroll
         for (int q = 0; q < R; ++q) {
-            sv[q] = spmv(q, p[q]);
+            sv[q] = spmv(q, p[q], P_);
             dl += p[q] * sv[q];
         }
         block_sum3<NT>(rz, bb, dl, red, phase);
@@ -381,7 +419,7 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
             float w[R];
 #pragma unroll
             for (int q = 0; q < R; ++q) {
-                w[q] = spmv(q, ap[q]);
+                w[q] = spmv(q, ap[q], P_);
                 gn += r[q] * ap[q];
                 de += w[q] * ap[q];
                 rr += r[q] * r[q];
@@ -410,6 +448,92 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
                 sv[q] = w[q] + beta * sv[q];
             }
             GLL_TRACE_CYC(15);
+        }
+        } else {
+        // Pipelined PCG (Ghysels & Vanroose 2014, preconditioned form): m = M^-1 w and n = A m
+        // by recurrence-free products, z, q, s, p by recurrences.  The reduction of
+        // (r,u), (w,u), (r,r) and the SpMV of m do not depend on each other, so one barrier
+        // per iteration publishes both; the LDS totals are read while the gathers are in
+        // flight.  The gathered vector is double-buffered: a fast wave may publish m_{i+1}
+        // while a slow one still gathers m_i.
+        float* Pb0 = P_;
+        float* Pb1 = P_ + mp4;
+        float w[R], z[R], qv[R], sv[R], mv[R];
+        float gl = 0.f, dl = 0.f, rl = 0.f;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            ap[q] = p[q];                      // u0 = M^-1 r0, published in Pb0 above
+            p[q] = z[q] = qv[q] = sv[q] = 0.f;
+            w[q] = spmv(q, ap[q], Pb0);        // w0 = A u0
+            mv[q] = mi[q] * w[q];
+            const int u = urow[q];
+            if (u < m) Pb1[u] = mv[q];
+            gl += r[q] * ap[q];
+            dl += w[q] * ap[q];
+            rl += r[q] * r[q];
+        }
+        GLL_TRACE_PT(3);
+        const float* qred = block_sum3_post<NT>(gl, dl, rl, red, phase);
+        int cur = 1;
+        float tol2 = 0.f, gam = 0.f, alpha = 0.f;
+        conv = false;
+        while (true) {
+            GLL_TRACE_CYC(10);
+            block_sum3_read<NT>(qred, gl, dl, rl);   // gamma_i, delta_i, |r_i|^2
+            const float* Pc = cur ? Pb1 : Pb0;
+            float nv[R];
+#pragma unroll
+            for (int q = 0; q < R; ++q) nv[q] = spmv(q, mv[q], Pc);   // n_i = A m_i
+            GLL_TRACE_CYC(11);
+            if (it == 0) {
+                tol2 = rtol * rtol * rl;
+                if (!(rl > 0.f)) {
+                    conv = true;
+                    break;
+                }
+            } else if (rl <= tol2) {
+                conv = true;
+                break;
+            }
+            if (it >= max_iter) break;
+            float beta, a;
+            if (it == 0) {
+                if (!(dl > 0.f)) break;   // breakdown before the first step
+                beta = 0.f;
+                a = gl / dl;
+            } else {
+                beta = gl * __builtin_amdgcn_rcpf(gam);
+                const float den = alpha * dl - beta * gl;
+                if (!(den > 0.f)) break;   // breakdown or NaN: reported as non-converged
+                a = (gl * alpha) * __builtin_amdgcn_rcpf(den);
+            }
+            ++it;
+            gam = gl;
+            alpha = a;
+            float* Pn = cur ? Pb0 : Pb1;
+            gl = dl = rl = 0.f;
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                z[q] = nv[q] + beta * z[q];
+                qv[q] = mv[q] + beta * qv[q];
+                sv[q] = w[q] + beta * sv[q];
+                p[q] = ap[q] + beta * p[q];
+                x[q] += a * p[q];
+                r[q] -= a * sv[q];
+                ap[q] -= a * qv[q];
+                w[q] -= a * z[q];
+                mv[q] = mi[q] * w[q];
+                const int u = urow[q];
+                if (u < m) Pn[u] = mv[q];
+                gl += r[q] * ap[q];
+                dl += w[q] * ap[q];
+                rl += r[q] * r[q];
+            }
+            GLL_TRACE_CYC(12);
+            qred = block_sum3_post<NT>(gl, dl, rl, red, phase);
+            cur ^= 1;
+            GLL_TRACE_CYC(13);
+        }
         }
     } else {
     block_sum2<NT>(rz, bb, red, phase);
@@ -603,11 +727,11 @@ __global__ __launch_bounds__(NT) void cg_lds_kernel(
 }
 
 
-template <int NT, int R, int S, typename TB, bool CGC>
+template <int NT, int R, int S, typename TB, int MODE>
 static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* b, size_t bs,
                           double* out64, float* out32, float rtol, int max_iter,
                           int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
-    size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4;
+    size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4 * (MODE == 2 ? 2 : 1);
     // entries past the ELL slices are compacted into LDS up to kOvfLds of them, the rest read
     // from the CSR; batched launches cap them so 4 workgroups still share a CU (a full-LDS
     // request would pin one per CU); a single graph's C workgroups take all the LDS there is
@@ -624,7 +748,7 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
         if (getenv("GLL_DEBUG")) fprintf(stderr, "gll: run_ell S=%d but ELL width %d\n", S, L.SE);
         return hipErrorInvalidValue;
     }
-    auto fn = cg_ell_kernel<NT, R, S, TB, CGC>;
+    auto fn = cg_ell_kernel<NT, R, S, TB, MODE>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
     launch_k(fn, dim3(L.C, bt.B), NT, lds, s, 
         L.m, L.C, L.base, L.at<int32_t>(ws, L.row_start), L.at<int32_t>(ws, L.row_len),
@@ -650,12 +774,15 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
         return launch_cg_grid_luu(L, ws, b, b_dtype, out64, out32, rtol, 0.f, max_iter,
                                   st_nonconv, st_iters, s);
     }
-#define GLL_ELL(NT, R, S)                                                                     \
-    return (L.flags & GLL_FLAG_CG_CLASSIC)                                                    \
-               ? run_ell<NT, R, S, TB, false>(L, bt, ws, b, bs, out64, out32, rtol, max_iter, \
-                                              st_nonconv, st_iters, s)                        \
-               : run_ell<NT, R, S, TB, true>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,  \
-                                             st_nonconv, st_iters, s)
+#define GLL_ELL(NT, R, S)                                                                   \
+    return (L.flags & GLL_FLAG_CG_CLASSIC)                                                  \
+               ? run_ell<NT, R, S, TB, 0>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
+                                          st_nonconv, st_iters, s)                          \
+           : (L.flags & GLL_FLAG_CG_PIPE)                                                   \
+               ? run_ell<NT, R, S, TB, 2>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
+                                          st_nonconv, st_iters, s)                          \
+               : run_ell<NT, R, S, TB, 1>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
+                                          st_nonconv, st_iters, s)
     if (m <= 64) GLL_ELL(64, 1, 24);
     if (m <= 128) GLL_ELL(128, 1, 24);
     if (m <= 256) GLL_ELL(256, 1, 24);
