@@ -98,20 +98,15 @@ inline int ell_slots(int m) {
 #define GLL_TRACE_EXIT(k) do {} while (0)
 #endif
 
-// Split of the Gram contraction over workgroups: each of KS workgroups of a 64x64 tile takes
-// a contiguous slice of the features and writes its own partial plane of D2; the select
-// kernel sums the planes in a fixed order.  Measured on MI355X at NS (tools/dispatch_probe.py,
-// profiles/r01_gram_dispatch.txt): a tile runs ~2 us per 64-deep chunk on one CU
-// (MFMA-bound), and KS = 2 / 4 overflow the 256 CUs into extra rounds (21.5 / 23.5 us against
-// 16.9 us for KS = 1), so even splits never pay; KS stays 1 until a balanced (stream-K)
-// schedule replaces them.
+// D2 planes.  A single small graph (T = ceil(n / 64) <= 16 tiles a side, 256 < d <= 512)
+// runs the split-phase Gram (gram_bf3s_kernel): T^2 workgroups, each off-diagonal tile as two
+// feature-phase halves writing partial planes that the select kernel adds in a fixed order.
+// Batches already fill the chip and keep one plane (the layout still reserves two, which is
+// 4 MB a graph at most).  (Evenly split fp32 tiles were measured before: 21.5 / 23.5 us for
+// KS = 2 / 4 against 16.9 us unsplit, profiles/r01_gram_dispatch.txt -- 2 T(T+1)/2
+// workgroups overflow the 256 CUs; T^2 does not.)
 inline int gram_splits(int n, int d) {
-#ifdef GLL_TRACE
-    if (const char* e = getenv("GLL_GRAM_KS")) return atoi(e);   // diagnostic sweeps only
-#endif
-    (void)n;
-    (void)d;
-    return 1;
+    return ((n + 63) / 64 <= 16 && d > 256 && d <= 512) ? 2 : 1;
 }
 
 size_t grid_cg_workspace_floats(int m, int C);
@@ -180,6 +175,12 @@ struct Layout {
     template <typename T>
     T* at(void* ws, size_t o) const { return reinterpret_cast<T*>(static_cast<char*>(ws) + o); }
 };
+
+// Planes the Gram kernel of a launch over B graphs writes (= planes the select kernel sums).
+inline int gram_planes(const Layout& L, int B) {
+    if (L.flags & (GLL_FLAG_GRAM_F32 | GLL_FLAG_GRAM_NOSPLIT)) return 1;
+    return (L.KS == 2 && B == 1) ? 2 : 1;
+}
 
 // ---------------------------------------------------------------------------------------
 // Device helpers

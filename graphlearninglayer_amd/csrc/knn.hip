@@ -429,6 +429,96 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int kBP = 256;            // features per phase
 constexpr int kBS = kBP + 8;        // LDS plane row stride (bf16)
 
+// Epilogue of the 64-tile split-bf16 Gram: row norms (wave sums of the per-slot squares),
+// the 4 feature-quarter partials of each quadrant summed in LDS in a fixed order,
+// D2 = |a_i|^2 + |b_j|^2 - 2 <a_i, b_j> staged as a [64][65] tile, then the direct and mirrored
+// stores (a diagonal tile takes the upper triangle for both halves: D2 bitwise symmetric).
+// nrm_of(t) reads norm t (0..63 rows bi, 64..127 rows bj) out of sqp[slot][wave]; Dz, when
+// set, receives zeros at the direct positions (the unused plane of a split diagonal tile).
+template <typename NF>
+__device__ __forceinline__ void bf3_epilogue(const f32x16& acc, const float (&sq)[8], float* smem,
+                                             float (*sqp)[16], float* nrm, NF nrm_of, int bi,
+                                             int bj, int n, float* __restrict__ D2, int ld,
+                                             float* __restrict__ Dz) {
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int qd = w & 3, kq = w >> 2;
+    // row norms: slot s of wave w is tile row 16 s + w, its features spread over the wave
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const float t = wave_sum_dpp(sq[s]);
+        if (lane == 0) sqp[s][w] = t;
+    }
+    __syncthreads();   // fragment reads done: the planes become partial / tile space
+    // partial quadrant -> LDS part[kq][qd][32][33] (C layout: col = lane & 31,
+    // row = (e&3) + 8(e>>2) + 4h)
+    float* pw = smem + (kq * 4 + qd) * 32 * 33;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) pw[((e & 3) + 8 * (e >> 2) + 4 * h) * 33 + r] = acc[e];
+    if (tid < 128) nrm[tid] = nrm_of(tid);
+    __syncthreads();
+    // tile element (ti, tj..tj+3): sum of the 4 feature quarters, fixed order
+    const int ti = tid >> 4, tj = 4 * (tid & 15);
+    float v[4];
+    {
+        const int q = 2 * (ti >> 5) + (tj >> 5), rr = ti & 31;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int cc = (tj & 31) + e;
+            float t = 0.f;
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) t += smem[(k4 * 4 + q) * 32 * 33 + rr * 33 + cc];
+            v[e] = t;
+        }
+    }
+    __syncthreads();
+    float* tile = smem + 16 * 32 * 33;   // [64][65], past the partials
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[ti * 65 + tj + e] = nrm[ti] + nrm[64 + tj + e] - 2.f * v[e];
+    __syncthreads();
+    // direct orientation: row bi*64 + ti, columns bj*64 + tj .. +3; a diagonal tile takes the
+    // upper triangle for both halves so D2 stays bitwise symmetric
+    const int i = bi * 64 + ti;
+    if (i < n) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int jj = tj + e;
+            o[e] = (bi == bj && jj < ti) ? tile[jj * 65 + ti] : tile[ti * 65 + jj];
+        }
+        float* dst = D2 + size_t(i) * ld + bj * 64 + tj;
+        float* dz = Dz ? Dz + size_t(i) * ld + bj * 64 + tj : nullptr;
+        if (bj * 64 + tj + 4 <= n) {
+            *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
+            if (dz) *reinterpret_cast<f32x4*>(dz) = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (bj * 64 + tj + e < n) {
+                    dst[e] = o[e];
+                    if (dz) dz[e] = 0.f;
+                }
+        }
+    }
+    // mirrored orientation: row bj*64 + ti, columns bi*64 + tj .. +3 from the tile's column ti
+    const int jr = bj * 64 + ti;
+    if (bi != bj && jr < n) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = tile[(tj + e) * 65 + ti];
+        float* dst = D2 + size_t(jr) * ld + bi * 64 + tj;
+        if (bi * 64 + tj + 4 <= n) {
+            *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (bi * 64 + tj + e < n) dst[e] = o[e];
+        }
+    }
+}
+
 template <bool VEC>
 __global__ __launch_bounds__(1024) void gram_bf3_kernel(const float* __restrict__ X, int n, int d,
                                                         int T, float* __restrict__ D2, int ld,
@@ -534,75 +624,121 @@ __global__ __launch_bounds__(1024) void gram_bf3_kernel(const float* __restrict_
         }
     }
     GLL_TRACE_PT(12);
-    // row norms: slot s of wave w is tile row 16 s + w, its features spread over the wave
+    bf3_epilogue(acc, sq, smem, sqp, nrm, [&](int t) { return sqp[t >> 4][t & 15]; }, bi, bj, n,
+                 D2, ld, nullptr);
+    GLL_TRACE_PT(14);
+}
+
+// K1a' (one graph, n <= 1024, 256 < d <= 512): the same tile over HALF the features.  With
+// T = ceil(n / 64) <= 16 the T (T + 1) / 2 upper-triangle tiles leave CUs idle (136 of 256 at
+// NS) while each tile pulls 256 KiB through one CU, and that pull is what bounds the kernel
+// (load_probe above).  Here each off-diagonal tile runs as two workgroups -- feature phase 0
+// into plane 0, phase 1 into plane 1 -- and each diagonal tile as one workgroup that loads its
+// 64 rows once for both phases (LDS rows 0..63: phase 0, rows 64..127: phase 1).  That is T^2
+// workgroups with 128 KiB of loads each; the select kernel adds the two planes in a fixed order
+// (NP = 2) and a diagonal tile writes zeros into plane 1.  Partial planes carry partial norms,
+// |a|^2_s + |b|^2_s - 2 <a, b>_s, so the plane sum is D2.
+template <bool VEC>
+__global__ __launch_bounds__(1024) void gram_bf3s_kernel(const float* __restrict__ X, int n,
+                                                         int d, int T, float* __restrict__ D2,
+                                                         int ld, size_t plane,
+                                                         int32_t* __restrict__ status,
+                                                         int32_t* __restrict__ rev_cnt,
+                                                         size_t xs, size_t wss) {
+    X = gshift_br(X, xs);
+    D2 = gshift_br(D2, wss);
+    status = gshift_br(status, wss);
+    rev_cnt = gshift_br(rev_cnt, wss);
+    constexpr int kPlane = 128 * kBS;
+    __shared__ __attribute__((aligned(16))) __bf16 smem_h[2 * kPlane];
+    __shared__ float sqp[8][16];
+    __shared__ float nrm[128];
+    float* smem = reinterpret_cast<float*>(smem_h);
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int b = xcd_tile(blockIdx.x, gridDim.x);
+    const bool dg = b < T;   // block-uniform
+    int bi = b, bj = b, half = 0;
+    if (!dg) {   // strictly-upper tile (b - T) / 2, row-major; half = feature phase = plane
+        int rem = (b - T) >> 1;
+        half = (b - T) & 1;
+        bi = 0;
+        while (rem >= T - 1 - bi) {
+            rem -= T - 1 - bi;
+            ++bi;
+        }
+        bj = bi + 1 + rem;
+    }
+    {   // per-call reset of the counters the select kernel accumulates into
+        const int g = blockIdx.x * 1024 + tid;
+        if (g < GLL_ST_NWORDS) status[g] = 0;
+        for (int q = g; q < n; q += gridDim.x * 1024) rev_cnt[q] = 0;
+    }
+    const int fo = 4 * lane;
+    // slot s -> LDS row 16 s + w.  Off-diagonal: tile row 16 s + w (0..63 rows bi, 64..127
+    // rows bj), features of phase `half`.  Diagonal: row bi*64 + 16 (s & 3) + w, phase s >> 2.
+    f32x4 v[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-        const float t = wave_sum_dpp(sq[s]);
-        if (lane == 0) sqp[s][w] = t;
+        const int R = dg ? 16 * (s & 3) + w : 16 * s + w;
+        const int row = R < 64 ? bi * 64 + R : bj * 64 + R - 64;
+        const int k = (dg ? (s >> 2) : half) * kBP + fo;
+        v[s] = load4_raw<VEC>(X + size_t(row < n ? row : n - 1) * d, k, d);
     }
-    __syncthreads();   // fragment reads done: the planes become partial / tile space
-    // partial quadrant -> LDS part[kq][qd][32][33] (C layout: col = lane & 31,
-    // row = (e&3) + 8(e>>2) + 4h)
-    float* pw = smem + (kq * 4 + qd) * 32 * 33;
+    float sq[8];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) pw[((e & 3) + 8 * (e >> 2) + 4 * h) * 33 + r] = acc[e];
-    if (tid < 128) nrm[tid] = sqp[tid >> 4][tid & 15];
-    __syncthreads();
-    // tile element (ti, tj..tj+3): sum of the 4 feature quarters, fixed order
-    const int ti = tid >> 4, tj = 4 * (tid & 15);
-    float v[4];
-    {
-        const int q = 2 * (ti >> 5) + (tj >> 5), rr = ti & 31;
+    for (int s = 0; s < 8; ++s) {
+        const int k = (dg ? (s >> 2) : half) * kBP + fo;
+        const f32x4 f = mask4<VEC>(v[s], k, d);
+        sq[s] = f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+        bf16x4 hv, lv;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int cc = (tj & 31) + e;
-            float t = 0.f;
-#pragma unroll
-            for (int k4 = 0; k4 < 4; ++k4) t += smem[(k4 * 4 + q) * 32 * 33 + rr * 33 + cc];
-            v[e] = t;
+            const __bf16 hb = static_cast<__bf16>(f[e]);
+            hv[e] = hb;
+            lv[e] = static_cast<__bf16>(f[e] - static_cast<float>(hb));
         }
+        const int o = (16 * s + w) * kBS + fo;
+        *reinterpret_cast<bf16x4*>(smem_h + o) = hv;
+        *reinterpret_cast<bf16x4*>(smem_h + kPlane + o) = lv;
     }
     __syncthreads();
-    float* tile = smem + 16 * 32 * 33;   // [64][65], past the partials
+    f32x16 acc;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) tile[ti * 65 + tj + e] = nrm[ti] + nrm[64 + tj + e] - 2.f * v[e];
-    __syncthreads();
-    GLL_TRACE_PT(13);
-    // direct orientation: row bi*64 + ti, columns bj*64 + tj .. +3; a diagonal tile takes the
-    // upper triangle for both halves so D2 stays bitwise symmetric
-    const int i = bi * 64 + ti;
-    if (i < n) {
-        float o[4];
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    const int qd = w & 3, kq = w >> 2;
+    const int qa = qd >> 1, qb = qd & 1;
+    auto mfma3 = [&](int oa, int ob) {
+        const bf16x8 ha = *reinterpret_cast<const bf16x8*>(smem_h + oa);
+        const bf16x8 la = *reinterpret_cast<const bf16x8*>(smem_h + kPlane + oa);
+        const bf16x8 hb = *reinterpret_cast<const bf16x8*>(smem_h + ob);
+        const bf16x8 lb = *reinterpret_cast<const bf16x8*>(smem_h + kPlane + ob);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(la, hb, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha, lb, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha, hb, acc, 0, 0, 0);
+    };
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int jj = tj + e;
-            o[e] = (bi == bj && jj < ti) ? tile[jj * 65 + ti] : tile[ti * 65 + jj];
-        }
-        float* dst = D2 + size_t(i) * ld + bj * 64 + tj;
-        if (bj * 64 + tj + 4 <= n) {
-            *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
+    for (int st = 0; st < 4; ++st) {
+        const int kk = 64 * kq + 16 * st + 8 * h;
+        if (dg) {   // both operands from the tile's own rows, phase 0 then phase 1
+            mfma3((32 * qa + r) * kBS + kk, (32 * qb + r) * kBS + kk);
+            mfma3((64 + 32 * qa + r) * kBS + kk, (64 + 32 * qb + r) * kBS + kk);
         } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (bj * 64 + tj + e < n) dst[e] = o[e];
+            mfma3((32 * qa + r) * kBS + kk, (64 + 32 * qb + r) * kBS + kk);
         }
     }
-    // mirrored orientation: row bj*64 + ti, columns bi*64 + tj .. +3 from the tile's column ti
-    const int jr = bj * 64 + ti;
-    if (bi != bj && jr < n) {
-        float o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = tile[(tj + e) * 65 + ti];
-        float* dst = D2 + size_t(jr) * ld + bi * 64 + tj;
-        if (bi * 64 + tj + 4 <= n) {
-            *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (bi * 64 + tj + e < n) dst[e] = o[e];
-        }
-    }
-    GLL_TRACE_PT(14);
+    if (dg)   // norm of row t: its phase-0 slot plus its phase-1 slot, both halves the same rows
+        bf3_epilogue(acc, sq, smem, sqp, nrm,
+                     [&](int t) {
+                         const int u = t & 63;
+                         return sqp[u >> 4][u & 15] + sqp[(u >> 4) + 4][u & 15];
+                     },
+                     bi, bj, n, D2, ld, D2 + plane);
+    else
+        bf3_epilogue(acc, sq, smem, sqp, nrm, [&](int t) { return sqp[t >> 4][t & 15]; }, bi, bj,
+                     n, D2 + size_t(half) * plane, ld, nullptr);
 }
 
 // --------------------------------------------------------------------------------------
@@ -1259,21 +1395,37 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
 // Wide 128-tiles when there are enough of them to fill the chip twice over (large graphs and
 // batches); the 64-tile kernel otherwise (a single NS graph has only 36 wide tiles).
 static bool use_wide_gram(const Layout& L, const Batch& bt) {
-    if (L.KS != 1 || (L.flags & GLL_FLAG_GRAM_NARROW)) return false;
+    if (gram_planes(L, bt.B) != 1 || (L.flags & GLL_FLAG_GRAM_NARROW)) return false;
     const int64_t T = (L.n + 127) / 128;
     return int64_t(bt.B) * T * (T + 1) / 2 >= 512;
 }
 
 // 48-tiles when 64-tiles would leave a quarter of the CUs idle and 48-tiles fit in one round.
 static bool use_gram48(const Layout& L, const Batch& bt) {
-    if (L.KS != 1 || (L.flags & GLL_FLAG_GRAM_NARROW)) return false;
+    if (gram_planes(L, bt.B) != 1 || (L.flags & GLL_FLAG_GRAM_NARROW)) return false;
     const int64_t T64 = (L.n + 63) / 64, T48 = (L.n + 47) / 48;
     return int64_t(bt.B) * T64 * (T64 + 1) / 2 < 192 && int64_t(bt.B) * T48 * (T48 + 1) / 2 <= 256;
 }
 
 hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
                        hipStream_t s) {
-    if (L.KS == 1 && !(L.flags & GLL_FLAG_GRAM_F32) && !(L.flags & GLL_FLAG_GRAM_NARROW)) {
+    const int planes = gram_planes(L, bt.B);
+    if (planes == 2) {
+        const int T = (L.n + 63) / 64;
+        const dim3 grid(T * T, bt.B);
+        float* D2 = L.at<float>(ws, L.D2);
+        const size_t plane = size_t(L.n) * L.ldD;
+        int32_t* st = L.at<int32_t>(ws, L.status);
+        int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
+        prof_begin(GLL_K_GRAM, s);
+        if (vec)
+            launch_k(gram_bf3s_kernel<true>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, plane, st, rc, bt.x, bt.ws);
+        else
+            launch_k(gram_bf3s_kernel<false>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, plane, st, rc, bt.x, bt.ws);
+        prof_end(GLL_K_GRAM, s);
+        return launch_status("knn.hip:launch_gram(bf3s)");
+    }
+    if (!(L.flags & GLL_FLAG_GRAM_F32) && !(L.flags & GLL_FLAG_GRAM_NARROW)) {
         const int T = (L.n + 127) / 128;
         if (int64_t(bt.B) * T * (T + 1) / 2 >= 512) {   // enough 128-tiles to fill the chip twice
             const dim3 grid(T * (T + 1) / 2, bt.B);
@@ -1289,7 +1441,7 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
             return launch_status("knn.hip:launch_gram(bf3w)");
         }
     }
-    if (L.KS == 1 && !(L.flags & GLL_FLAG_GRAM_F32)) {
+    if (!(L.flags & GLL_FLAG_GRAM_F32)) {
         const int T = (L.n + 63) / 64;
         const dim3 grid(T * (T + 1) / 2, bt.B);
         float* D2 = L.at<float>(ws, L.D2);
@@ -1337,7 +1489,7 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
     }
     const int T = (L.n + 63) / 64;
     const int tiles = T * (T + 1) / 2;
-    const int KS = L.KS;
+    const int KS = planes;
     // slice of the features per split in whole 64-deep chunks, grouped NCH per super-chunk.
     // (128-deep chunks -- half the barriers -- measured no faster at NS, B = 64 or stress:
     // profiles/r01_gram_chunk_depth.txt; the template keeps the depth a parameter.)
@@ -1380,6 +1532,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     dim3 grid((n + 3) / 4, bt.B);
     prof_begin(GLL_K_SELECT, s);
     const size_t plane = size_t(n) * L.ldD;
+    const int planes = gram_planes(L, bt.B);
 #define GLL_SEL3(KCV, V, NPV)                                                                  \
     launch_k((bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2> : knn_select_kernel<KCV, V, NPV, 1>), grid, 256, 0, s,  \
         L.at<float>(ws, L.D2), L.ldD, plane, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0,     \
@@ -1389,8 +1542,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
         L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub, bt.x, bt.ws, bt.st)
 #define GLL_SEL(KCV, V)                                                                        \
     do {                                                                                       \
-        if (L.KS == 4) GLL_SEL3(KCV, V, 4);                                                    \
-        else if (L.KS == 2) GLL_SEL3(KCV, V, 2);                                               \
+        if (planes == 2) GLL_SEL3(KCV, V, 2);                                                  \
         else GLL_SEL3(KCV, V, 1);                                                              \
     } while (0)
     if (KC == 16) { if (vec) GLL_SEL(16, true); else GLL_SEL(16, false); }

@@ -48,6 +48,7 @@ extern "C" {
 #define GLL_FLAG_CG_PERCOL 8    /* single graphs with m > 1024: per-column CG instead of the whole-GPU CG (diagnostic) */
 #define GLL_FLAG_GRAM_F32 16    /* Gram on the fp32 MFMA kernels instead of the split-bf16 one (diagnostic) */
 #define GLL_FLAG_CG_PIPE 32     /* per-column CG: pipelined PCG (one barrier per iteration) (diagnostic) */
+#define GLL_FLAG_GRAM_NOSPLIT 64 /* small single graphs: unsplit Gram tiles (one D2 plane) (diagnostic) */
 
 typedef struct gll_problem {
     int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */
