@@ -149,6 +149,26 @@ def test_scalar_and_wide_feature_paths(d):
     assert O.rel_err(grad, O.backward(st, g)) < TOL
 
 
+@pytest.mark.parametrize("n,d,eps", [(777, 333, "auto"), (1024, 512, 1.0), (900, 300, 1.0),
+                                     (1025, 512, 1.0)])
+def test_split_phase_gram_shapes(n, d, eps):
+    """Single graphs with ceil(n/64) <= 16 and 256 < d <= 512 take the split-phase Gram (two
+    partial D2 planes, diagonal tiles zeroing plane 1 of an uninitialised workspace): ragged
+    tiles (777, 900), the largest split grid (1024 = 16 tiles), a scalar-load feature width (333)
+    and a half-empty second phase (300).  n = 1025 is the first shape past the split (17 tiles)."""
+    from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
+    base = n // 5
+    X, lab = synth(base, n - base, d, r=1.0, seed=11)
+    Y = one_hot(lab[:base])
+    g = seeded_gbar(n - base, 10, 3)
+    U, grad = _run(X, Y, 0.07, eps, 10, g)
+    ind = _gpu_knn(X, 10, eps)["knn_idx"].cpu().numpy()
+    assert O.knn_set_mismatch(X, ind, 10) == []
+    Uo, st = O.forward(X, Y, 0.07, eps, 10, knn=(ind, None))
+    assert O.rel_err(U, Uo) < TOL
+    assert O.rel_err(grad, O.backward(st, g)) < TOL
+
+
 def test_hub_row_longer_than_lds_chunk():
     """One point is a neighbour of everybody: its CSR row exceeds the 256-entry chunk."""
     rng = np.random.default_rng(0)
