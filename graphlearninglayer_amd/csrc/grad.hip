@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
         const int k = 4 * lane + 4 * kWave * q;
         const f32x4 r = csum * xv[q] - acc[q];
         if constexpr (VEC) {
-            if (k < d) *reinterpret_cast<f32x4*>(oi + k) = r;
+            if (k < d) __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(oi + k));   // streamed out: not re-read here
         } else {
             if (k + 0 < d) oi[k + 0] = r.x;
             if (k + 1 < d) oi[k + 1] = r.y;

@@ -491,8 +491,8 @@ __device__ __forceinline__ void bf3_epilogue(const f32x16& acc, const float (&sq
         float* dst = D2 + size_t(i) * ld + bj * 64 + tj;
         float* dz = Dz ? Dz + size_t(i) * ld + bj * 64 + tj : nullptr;
         if (bj * 64 + tj + 4 <= n) {
-            *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
-            if (dz) *reinterpret_cast<f32x4*>(dz) = f32x4{0.f, 0.f, 0.f, 0.f};
+            __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<f32x4*>(dst));
+            if (dz) __builtin_nontemporal_store(f32x4{0.f, 0.f, 0.f, 0.f}, reinterpret_cast<f32x4*>(dz));
         } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
@@ -510,7 +510,7 @@ __device__ __forceinline__ void bf3_epilogue(const f32x16& acc, const float (&sq
         for (int e = 0; e < 4; ++e) o[e] = tile[(tj + e) * 65 + ti];
         float* dst = D2 + size_t(jr) * ld + bi * 64 + tj;
         if (bi * 64 + tj + 4 <= n) {
-            *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
+            __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<f32x4*>(dst));
         } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e)

@@ -1,6 +1,6 @@
 """A/B of gll_problem.flags variants through the raw C ABI (diagnostic, run on the GPU box).
 
-    python tools/ab_flags.py [--flags 0,4] [--configs ns,stress] [--batch 1,64]
+    python tools/ab_flags.py [--flags 0,4] [--configs ns,stress] [--batch 1,64] [--lib PATH]
 
 For each config x batch x flags: mean launch time of every kernel (HIP events around each
 launch), wall time per fwd+bwd with nothing else on the host path, CG iterations, and the
@@ -25,8 +25,11 @@ ap.add_argument("--flags", default="0,4")
 ap.add_argument("--configs", default="ns")
 ap.add_argument("--batch", default="1,64")
 ap.add_argument("--reps", type=int, default=50)
+ap.add_argument("--lib", default="", help="another build of libgll.so to load instead (A/B of builds)")
 a = ap.parse_args()
 
+if a.lib:
+    _lib._lib = _lib._declare(ct.CDLL(os.path.abspath(a.lib)))
 lib = _lib.lib()
 names = [_lib.kernel_name(q) for q in range(_lib.K_COUNT)]
 s = torch.cuda.current_stream().cuda_stream
