@@ -435,6 +435,10 @@ constexpr int kBS = kBP + 8;        // LDS plane row stride (bf16)
 // stores (a diagonal tile takes the upper triangle for both halves: D2 bitwise symmetric).
 // nrm_of(t) reads norm t (0..63 rows bi, 64..127 rows bj) out of sqp[slot][wave]; Dz, when
 // set, receives zeros at the direct positions (the unused plane of a split diagonal tile).
+// The full-width stores are non-temporal: D2 is read once, by the select kernel on other XCDs,
+// and streaming it out leaves less for the end-of-kernel L2 write-back (NS call 71.4 -> 70.5 us
+// over 300 calls, alternating builds, tools/ab_flags.py --lib; on the 128-tile kernel the same
+// change measured +0.6% at stress and -1.3% at B = 64, so that one keeps ordinary stores).
 template <typename NF>
 __device__ __forceinline__ void bf3_epilogue(const f32x16& acc, const float (&sq)[8], float* smem,
                                              float (*sqp)[16], float* nrm, NF nrm_of, int bi,
