@@ -1160,6 +1160,21 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_max_u32(uint32_t v) {
+    const uint32_t o = __builtin_amdgcn_update_dpp(0u, v, CTRL, ROW_MASK, 0xf, false);
+    return o > v ? o : v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    v = dpp_max_u32<0xB1, 0xf>(v);
+    v = dpp_max_u32<0x4E, 0xf>(v);
+    v = dpp_max_u32<0x141, 0xf>(v);
+    v = dpp_max_u32<0x140, 0xf>(v);
+    v = dpp_max_u32<0x142, 0xa>(v);
+    v = dpp_max_u32<0x143, 0xc>(v);
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 // Exact merge (fallback): round t hands the t-th smallest (d2, index) key to lane t.
 template <int KC>
 __device__ __forceinline__ int merge_exact(uint64_t (&key)[KC], int kc) {
@@ -1216,7 +1231,12 @@ __device__ __forceinline__ bool merge_threshold(const uint64_t (&key)[KS], int k
         for (int s = 0; s < KS; ++s) c += __popcll(__ballot(hv[s] <= t));
         return c;
     };
-    uint32_t lo = 0u, up = 0xFFFFFFFEu;
+    // T lies between the smallest list head and, when at least kc entries are that small, the
+    // largest head: a bracket of ~2^24 instead of 2^32 (8 fewer steps at NS)
+    uint32_t lo = wave_min_u32(hv[0]), up = 0xFFFFFFFEu;
+    const uint32_t hmax = wave_max_u32(hv[0] == 0xFFFFFFFFu ? 0u : hv[0]);
+    if (lo > up) lo = up;   // every list empty
+    if (hmax >= lo && count_le(hmax) >= kc) up = hmax;
     if (count_le(up) >= kc) {
         while (lo < up) {   // smallest T with count_le(T) >= kc (wave-uniform, <= 32 steps)
             const uint32_t mid = lo + ((up - lo) >> 1);
