@@ -3,6 +3,13 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config ns|fullysup|stress|plumbing]
     torchrun --nproc-per-node N bench.py --gpus N ...        (one process per GPU)
 
+`--gpus N` with N > 1 and no WORLD_SIZE in the environment starts the N ranks itself: it runs
+`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...` as a child
+process before anything touches the GPU and exits with the child's status (rank 0's JSON
+line is the child's stdout).  Under an outer launcher WORLD_SIZE must equal N.
+`--dry-run` replaces the GPU leg by a CPU stand-in step over gloo, so the launcher, the
+coalesced prediction gather and the max-over-ranks timing can be tested on a CPU box.
+
 One step = one `LaplaceLearningSparseHard.apply` forward (kNN graph built from scratch)
 + the backward of a fixed seeded upstream gradient dL/dU, on the rank's own synthetic
 minibatch graph (seed = rank; SURVEY.md §8d generator), plus the asynchronous RCCL
@@ -16,6 +23,8 @@ import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -57,7 +66,31 @@ def parse():
     ap.add_argument("--batch", type=int, default=64,
                     help="graphs per launch of the batched entry point measured beside the "
                          "headline (SURVEY.md §8f-2); 0 disables")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU stand-in step over gloo instead of the GPU path (launcher and "
+                         "gather test; the JSON line is marked dry_run and is no measurement)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(a) -> int:
+    """Start `a.gpus` ranks of this script under torch.distributed.run (one process per GPU,
+    RCCL over xGMI) and return the launcher's exit status.  Runs before any GPU call: this
+    process only waits for its child."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this host driver
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
 
 
 def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps):
@@ -186,8 +219,36 @@ def c_abi_measure(X, Y, tau, eps, k, gbar, steps, warmup):
                     "no torch autograd engine on the host path"}
 
 
-def cpu_baseline(cfg, eps, tau, seconds):
-    """Time the reference's CPU step sequence (oracle/gll_port.py, 'port') on this host."""
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def _port_calibration():
+    """Port-vs-reference time ratio measured in the build container, where the reference
+    itself can run (tools/calibrate_port.py -> profiles/*_port_calibration.json)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_port_calibration.json")))
+    if not paths:
+        return None
+    with open(paths[-1]) as f:
+        doc = json.load(f)
+    doc["file"] = os.path.relpath(paths[-1], ROOT)
+    return doc
+
+
+def cpu_baseline(cfg, eps, tau, seconds, config_name):
+    """Time the reference's CPU step sequence (oracle/gll_port.py, 'port') on this host.
+
+    Threads: torch's intra-op pool as the box sets it (OMP_NUM_THREADS = 16 = this job's CPU
+    share on the GPU box, whatever nproc says); the port is mostly single-threaded anyway
+    (SuperLU, scipy, the Python loop), like the reference."""
     from oracle import gll_port
 
     X, lab = synth(cfg["base"], cfg["batch"], cfg["d"], r=cfg["r"], seed=0)
@@ -202,19 +263,93 @@ def cpu_baseline(cfg, eps, tau, seconds):
         gll_port.backward(saved, g)
         times.append(time.perf_counter() - t0)
     med = float(np.median(times))
-    return {"value": round(1.0 / med, 3), "unit": "calls/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"{len(times)} fwd+bwd calls of oracle/gll_port.py (reference step "
-                      f"sequence: exact kNN + scipy CSR + SuperLU + torch sparse mm) on "
-                      f"{cfg['base']}+{cfg['batch']}x{cfg['d']} k={cfg['k']}, median",
-            "host": platform.processor() or platform.machine(), "nproc": os.cpu_count()}
+    out = {"value": round(1.0 / med, 3), "unit": "calls/s", "cores": torch.get_num_threads(),
+           "kind": "port",
+           "sample": f"{len(times)} fwd+bwd calls of oracle/gll_port.py (reference step "
+                     f"sequence: exact kNN + scipy CSR + SuperLU + torch sparse mm) on "
+                     f"{cfg['base']}+{cfg['batch']}x{cfg['d']} k={cfg['k']}, median",
+           "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+           "threads_note": ("torch intra-op threads = OMP_NUM_THREADS "
+                            f"({os.environ.get('OMP_NUM_THREADS', 'unset')}), the job's CPU share "
+                            "on the GPU box; nproc counts the whole host")}
+    cal = _port_calibration()
+    if cal is not None and config_name in cal.get("configs", {}):
+        cc = cal["configs"][config_name]
+        out["port_vs_reference"] = {
+            "ratio_ref_over_port": cc["ratio_ref_over_port"],
+            "port_ms": cc["port_ms"], "reference_ms": cc["reference_ms"],
+            "where": cal.get("host", "build container"), "source": cal["file"],
+            "reference_equiv_calls_s": round(out["value"] / cc["ratio_ref_over_port"], 3),
+            "note": "reference = /root/reference/GLL.py with the exact graphlearning stand-in, "
+                    "timed beside the port in the build container (the reference cannot travel "
+                    "to the GPU box); reference_equiv = this box's port rate / ratio"}
+    return out
+
+
+def dry_run(a, world, rank):
+    """CPU stand-in for the GPU leg (no measurement): the same launcher, warm-up/timed split,
+    coalesced gather and max-over-ranks reduction, with a tiny deterministic CPU step whose
+    'predictions' identify the rank, so the gathers can be checked for rank order."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    c = dict(CONFIGS["plumbing"])
+    m = c["batch"]
+    base_u = torch.arange(m * 10, dtype=torch.float64).reshape(m, 10) / (m * 10)
+    gatherer = PredictionGatherer(every=GATHER_EVERY)
+
+    def step(s):
+        U = base_u + rank + 1000.0 * s
+        gatherer.add(U)
+        return U
+
+    for s in range(a.warmup):
+        step(s)
+    gatherer.wait()
+    gatherer.gathered = []
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for s in range(a.steps):
+        step(a.warmup + s)
+    gatherer.wait()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ok = True
+    if world > 1:
+        full = torch.cat([blk.transpose(0, 1) for blk in gatherer.gathered])   # (calls, world, m, C)
+        for s in range(a.steps):
+            for r in range(world):
+                ok &= bool(torch.equal(full[s, r], base_u + r + 1000.0 * (a.warmup + s)))
+        ok &= full.shape[0] == a.steps
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "dry_run": True, "unit": "calls/s",
+                          "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": round(1e3 * elapsed / max(a.steps, 1), 4),
+                          "gather_check": "ok" if ok else "FAILED",
+                          "config": {"workload": "dry-run stand-in", "parallelism": f"dp{world}"}}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if ok else 1
 
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch(a)          # N ranks, one per GPU; nothing here has touched the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if a.dry_run:
+        return dry_run(a, world, rank)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -230,7 +365,7 @@ def main():
     gbar = torch.from_numpy(seeded_gbar(c["batch"], 10, 1234 + rank)).to(dev)
     lap = GLL.LaplaceLearningSparseHard.apply
 
-    gatherer = PredictionGatherer(every=GATHER_EVERY)
+    gatherer = PredictionGatherer(every=GATHER_EVERY, keep=1)
 
     def step():
         U = lap(X, Y, tau, eps, k)
@@ -282,6 +417,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    gather_check = None
+    if world > 1:
+        # every rank's inputs are fixed, so each slot of the last gathered group must hold
+        # that rank's U: compare per-rank checksums (one tiny all_gather, outside the timing)
+        own = U.detach().double().sum().reshape(1)
+        sums = torch.empty(world, dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(sums, own)
+        blk = gatherer.gathered[-1].double().sum(dim=(2, 3))            # (world, calls)
+        gather_check = "ok" if torch.allclose(blk, sums[:, None].expand_as(blk),
+                                              rtol=1e-12, atol=0.0) else "FAILED"
+
     roofline = None
     call_roof_s = None
     if dominant is not None:
@@ -310,7 +456,10 @@ def main():
         f_knn = units["gram_d2_kernel"][1]
         b_rest = sum(w_ * per_kernel[kn]["launches_per_step"] for kn, (b_, w_) in units.items()
                      if b_ == "hbm" and kn in per_kernel)
-        call_roof_s = f_knn / (GRAM_ROOF_TFS * 1e12) + b_rest / (HBM_PEAK_GBS * 1e9)
+        call_roof_s = {  # SURVEY §8d prices the kNN at the fp32 MFMA peak; the split-bf16 roof
+                         # is what the Gram here actually runs on (both reported, labelled)
+            "fp32_mfma": f_knn / (MFMA_F32_PEAK_TFS * 1e12) + b_rest / (HBM_PEAK_GBS * 1e9),
+            "split_bf16": f_knn / (GRAM_ROOF_TFS * 1e12) + b_rest / (HBM_PEAK_GBS * 1e9)}
         for kn, v in per_kernel.items():
             b_, w_ = units[kn]
             v["algorithmic"] = (f"{w_ / 1e9:.4g} GFLOP" if b_ == "mfma" else f"{w_ / 1e6:.4g} MB")
@@ -325,7 +474,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
-        cpu = cpu_baseline(c, eps, tau, a.cpu_seconds)
+        cpu = cpu_baseline(c, eps, tau, a.cpu_seconds, a.config)
 
     if rank == 0:
         calls = world * a.steps
@@ -349,13 +498,22 @@ def main():
                                       if world > 1 else "none")},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "gather_check": gather_check,
             "kernels": per_kernel,
             "c_abi": c_abi,
             "batched": batched,
         }
         if roofline is not None:
-            out["call_roofline"] = {"t_roof_us": round(call_roof_s * 1e6, 3),
-                                    "frac": round(call_roof_s / (elapsed / a.steps), 5)}
+            step_s = elapsed / a.steps
+            out["call_roofline"] = {
+                "definition": "t_roof = F_kNN / MFMA peak + B_rest / 8 TB/s (SURVEY.md §8d), "
+                              "frac = t_roof / measured step time",
+                "sec8d_fp32_mfma": {"kNN_peak_TFs": MFMA_F32_PEAK_TFS,
+                                    "t_roof_us": round(call_roof_s["fp32_mfma"] * 1e6, 3),
+                                    "frac": round(call_roof_s["fp32_mfma"] / step_s, 5)},
+                "split_bf16": {"kNN_peak_TFs": round(GRAM_ROOF_TFS, 1),
+                               "t_roof_us": round(call_roof_s["split_bf16"] * 1e6, 3),
+                               "frac": round(call_roof_s["split_bf16"] / step_s, 5)}}
         if cpu:
             out["speedup_vs_cpu"] = round(out["value"] / cpu["value"], 1)
         print(json.dumps(out), flush=True)
@@ -387,4 +545,4 @@ def _cg_iters(X, Y, tau, eps, k, gbar):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -322,6 +322,7 @@ def device_graph(X: torch.Tensor, k: int = DEFAULT_K, epsilon="auto"):
             w=arr(view.w, span, torch.float32)[src],
             d2=arr(view.d2, span, torch.float32)[src],
             deg=arr(view.deg, n, torch.float32),
+            status=arr(view.status, _lib.ST_NWORDS, torch.int32),
             workspace=ws,
         )
     return out

@@ -18,10 +18,11 @@ FLAG_CG_GRID = 1   # gll_problem.flags: force the whole-GPU CG (include/gll.h)
 FLAG_GRAM_NARROW = 2   # gll_problem.flags: 64-tile Gram everywhere (diagnostic)
 FLAG_CG_CLASSIC = 4   # gll_problem.flags: two-reduction per-column PCG (diagnostic)
 FLAG_CG_PERCOL = 8   # gll_problem.flags: per-column CG for large single graphs (diagnostic)
-FLAG_GRAM_F32 = 16   # gll_problem.flags: fp32-MFMA Gram kernels (diagnostic)
+FLAG_GRAM_F32 = 16   # gll_problem.flags: retired (fp32-MFMA Gram kernels removed); rejected
 FLAG_CG_PIPE = 32    # gll_problem.flags: pipelined per-column PCG (diagnostic)
 FLAG_GRAM_NOSPLIT = 64   # gll_problem.flags: unsplit Gram tiles for small single graphs (diagnostic)
 ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
+ST_KNN_RESCAN = 5   # kNN rows re-ranked over every column under the Gram error bound
 ST_NWORDS = 16
 K_GRAM, K_SELECT, K_FINALIZE, K_CG, K_EDGE, K_GRAD = range(6)
 K_COUNT = 6

@@ -90,7 +90,8 @@ static int check(const gll_problem* p) {
     if (p->n < 2 || p->d < 1 || p->C < 1 || p->K < 2) return GLL_ERR_INVALID_ARG;
     if (p->base < 0 || p->base > p->n) return GLL_ERR_INVALID_ARG;
     const int K = p->K < p->n ? p->K : p->n;
-    if (K - 1 > 64) return GLL_ERR_UNSUPPORTED;      // candidate lists hold <= 64
+    if (K - 1 > kMaxKm1) return GLL_ERR_UNSUPPORTED;  // candidate lists + rescan lanes
+    if (p->flags & GLL_FLAG_GRAM_F32) return GLL_ERR_UNSUPPORTED;   // retired (round 2)
     if (p->C > 256) return GLL_ERR_UNSUPPORTED;       // rhs accumulators per lane
     if ((p->d + 255) / 256 > 16) return GLL_ERR_UNSUPPORTED;  // d <= 4096 in the SpMM
     if (int64_t(p->n) * K > INT32_MAX / 2) return GLL_ERR_UNSUPPORTED;

@@ -14,6 +14,7 @@
 namespace gll {
 
 constexpr int kWave = 64;
+constexpr int kMaxKm1 = 56;      // K - 1 <= 56: the kNN rescan keeps >= 8 lanes of a wave free
 
 // ---------------------------------------------------------------------------------------
 // Workspace layout.  One block per forward/backward pair, carved into 256-B aligned arrays.
@@ -178,7 +179,7 @@ struct Layout {
 
 // Planes the Gram kernel of a launch over B graphs writes (= planes the select kernel sums).
 inline int gram_planes(const Layout& L, int B) {
-    if (L.flags & (GLL_FLAG_GRAM_F32 | GLL_FLAG_GRAM_NOSPLIT)) return 1;
+    if (L.flags & GLL_FLAG_GRAM_NOSPLIT) return 1;
     return (L.KS == 2 && B == 1) ? 2 : 1;
 }
 

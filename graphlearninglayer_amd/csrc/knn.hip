@@ -1,20 +1,26 @@
 // knn.hip -- exact brute-force kNN for the GLL graph (replaces the annoy search of
 // graphlearning.weightmatrix.knnsearch, /root/reference/GLL.py:183).
 //
-//  K1a gram_lds_kernel  D2 = |x_i|^2 + |x_j|^2 - 2 X X^T on fp32 MFMA (v_mfma_f32_32x32x2_f32),
-//                       upper-triangle 64x64 tiles only (mirrored writes), split-K over two
-//                       wave groups, LDS-staged double-buffered k-chunks, row norms from the
-//                       same operands.
+//  K1a gram_bf3*_kernel D2 = |a_i|^2 + |a_j|^2 - 2 <a_i, a_j> on split-bf16 MFMA over the
+//                       rows centred on row 0 (a = x - x_0: distance-invariant, and it keeps
+//                       the product error proportional to the spread of the rows, not to
+//                       their offset), upper-triangle tiles only (mirrored writes).  D2 only
+//                       NOMINATES candidates.
 //  K1b knn_select_kernel one wave per row:
 //                       1. per-lane sorted candidate lists over the D2 row (16-B loads);
-//                       2. a 64-lane merge to kc = K-1+margin candidates, one DPP arg-min of
-//                          the packed (d2, index) key per round;
-//                       3. exact re-ranking with d^2 = sum_k (x_ik - x_jk)^2, eight candidates
-//                          at a time (8-lane groups, DPP group sums) -- bitwise symmetric in
-//                          (i, j) because both orders run the same lane mapping;
+//                       2. a threshold merge to kc = K-1+margin candidates (exact 64-bit
+//                          merge when a lane's list overflowed);
+//                       3. exact re-ranking with d^2 = sum_k (x_ik - x_jk)^2 in float64,
+//                          eight candidates at a time (8-lane groups, DPP group sums) --
+//                          bitwise symmetric in (i, j) because both orders run the same lane
+//                          mapping;
 //                       4. the K-1 nearest by (exact d^2, index); self forced to rank 0 with
 //                          distance 0 (the stand-in contract of SURVEY.md §8c);
-//                       5. every valid pair (i -> j) is pushed onto j's reverse list (or the
+//                       5. a certificate that no column left out of the candidates can beat
+//                          the (K-1)-th exact distance given the Gram's error bound, else an
+//                          exact re-rank of every column under the bound (rare; counted in
+//                          GLL_ST_KNN_RESCAN) -- the result is the exact kNN for any input;
+//                       6. every valid pair (i -> j) is pushed onto j's reverse list (or the
 //                          overflow list), which is how the symmetric union of GLL.py:197 is
 //                          built without an n x n structure or a prefix sum.
 #include <limits.h>
@@ -26,369 +32,6 @@
 namespace gll {
 
 GLL_TRACE_UNIT(knn)
-
-// --------------------------------------------------------------------------------------
-// K1a: symmetric Gram tile.  D2 is symmetric, so only tiles bi <= bj are computed and the
-// off-diagonal ones are written in both orientations.  Small problems have fewer tiles than
-// CUs, so the feature dimension is split over KS workgroups per tile (gram_splits): each
-// writes a partial plane  |a_i|^2_s + |b_j|^2_s - 2 <a_i, b_j>_s  over its slice s, and the
-// select kernel adds the planes in a fixed order -- no inter-workgroup synchronisation.
-//
-// 512 threads = 8 waves: wave (kh, qd) owns the 32x32 quadrant qd of the 64x64 tile and the
-// k-half kh of every 64-deep chunk (split-K inside the workgroup, halves combined in LDS in a
-// fixed order).  Operands stream through a register ring of NCH chunks: chunk c of the next
-// super-chunk is loaded into ring slot c right after slot c went to LDS, so a load has
-// NCH-1 chunks of MFMA work to hide behind; LDS is double-buffered per chunk.
-// --------------------------------------------------------------------------------------
-// k per LDS chunk: GK = 64 or 128 (template); rows padded to GK + 4 floats (conflict-free
-// ds_read_b128).  128-deep chunks halve the barriers per tile (one LDS turnaround each).
-constexpr int kGK = 64;
-
-// 16 MFMAs over 32 k: lane (r, h) holds A[r][8u + 4h + t], B[c=r][8u + 4h + t].  Two
-// independent accumulator chains (alternate u) -- with 2 waves per SIMD that keeps four
-// chains in flight per SIMD, what the fp32 MFMA needs to issue every 64 cycles.
-__device__ __forceinline__ void gram_chunk_mfma(const f32x4 (&a)[4], const f32x4 (&b)[4],
-                                                f32x16 (&acc)[2], float& sa, float& sb) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        sa += a[u].x * a[u].x + a[u].y * a[u].y + a[u].z * a[u].z + a[u].w * a[u].w;
-        sb += b[u].x * b[u].x + b[u].y * b[u].y + b[u].z * b[u].z + b[u].w * b[u].w;
-        f32x16& c = acc[u & 1];
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].x, b[u].x, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].y, b[u].y, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].z, b[u].z, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].w, b[u].w, c, 0, 0, 0);
-    }
-}
-
-template <bool VEC, int NCH, int GK>
-__global__ __launch_bounds__(512) void gram_lds_kernel(const float* __restrict__ X, int n, int d,
-                                                       int T, int KS, int kspan,
-                                                       float* __restrict__ D2, int ld,
-                                                       size_t plane,
-                                                       int32_t* __restrict__ status,
-                                                       int32_t* __restrict__ rev_cnt,
-                                                       size_t xs, size_t wss) {
-    GLL_TRACE_SCOPE(0);
-    X = gshift_br(X, xs);
-    D2 = gshift_br(D2, wss);
-    status = gshift_br(status, wss);
-    rev_cnt = gshift_br(rev_cnt, wss);
-    constexpr int kGL = GK + 4;
-    constexpr int CS = GK / 64;   // 64-column segments of a chunk row
-    // stage[buf][A|B][64 rows][kGL]; the epilogue reuses the same storage
-    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * 64 * kGL];
-    __shared__ float s_sq[2][64];
-    const int tid = threadIdx.x;
-    const int lane = lane_id();
-    const int wave = tid >> 6;
-    const int kh = wave >> 2;             // k-half of every chunk
-    const int qd = wave & 3;              // 32x32 quadrant of this wave
-    const int r = lane & 31, h = lane >> 5;
-    const int ks = blockIdx.x % KS;
-    int bi = 0, rem = blockIdx.x / KS;
-    while (rem >= T - bi) {
-        rem -= T - bi;
-        ++bi;
-    }
-    const int bj = bi + rem;
-    {   // per-call reset of the counters the select kernel accumulates into
-        const int g = blockIdx.x * 512 + tid;
-        if (g < GLL_ST_NWORDS) status[g] = 0;
-        for (int q = g; q < n; q += gridDim.x * 512) rev_cnt[q] = 0;
-    }
-    GLL_TRACE_PT(10);
-#ifdef GLL_TRACE
-    if (blockIdx.x == 0 && threadIdx.x == 0) g_trace[21] = __builtin_amdgcn_s_memtime();
-#endif
-    const int k_lo = ks * kspan;
-    const int k_hi = min(d, k_lo + kspan);
-    const int nsup = kspan / (GK * NCH);
-    // loader role: thread t moves float4 column 4 (t & 15) of rows (t >> 4) and (t >> 4) + 32
-    // of A and of B for every chunk
-    const int lrow = tid >> 4, lcol = 4 * (tid & 15);
-    const float* ga0 = X + size_t(min(bi * 64 + lrow, n - 1)) * d;
-    const float* ga1 = X + size_t(min(bi * 64 + lrow + 32, n - 1)) * d;
-    const float* gb0 = X + size_t(min(bj * 64 + lrow, n - 1)) * d;
-    const float* gb1 = X + size_t(min(bj * 64 + lrow + 32, n - 1)) * d;
-    f32x4 ring[NCH][4 * CS];
-    auto gload = [&](int chunk, f32x4 (&v)[4 * CS]) {   // raw: masked when stored to LDS
-#pragma unroll
-        for (int cs = 0; cs < CS; ++cs) {
-            const int k = k_lo + chunk * GK + cs * 64 + lcol;
-            v[4 * cs + 0] = load4_raw<VEC>(ga0, k, k_hi);
-            v[4 * cs + 1] = load4_raw<VEC>(ga1, k, k_hi);
-            v[4 * cs + 2] = load4_raw<VEC>(gb0, k, k_hi);
-            v[4 * cs + 3] = load4_raw<VEC>(gb1, k, k_hi);
-        }
-    };
-    auto lstore = [&](int chunk, int buf, const f32x4 (&v)[4 * CS]) {
-        float* A = smem + (buf * 2 + 0) * 64 * kGL;
-        float* B = smem + (buf * 2 + 1) * 64 * kGL;
-#pragma unroll
-        for (int cs = 0; cs < CS; ++cs) {
-            const int k = k_lo + chunk * GK + cs * 64 + lcol;
-            const int col = cs * 64 + lcol;
-            *reinterpret_cast<f32x4*>(A + lrow * kGL + col) = mask4<VEC>(v[4 * cs + 0], k, k_hi);
-            *reinterpret_cast<f32x4*>(A + (lrow + 32) * kGL + col) = mask4<VEC>(v[4 * cs + 1], k, k_hi);
-            *reinterpret_cast<f32x4*>(B + lrow * kGL + col) = mask4<VEC>(v[4 * cs + 2], k, k_hi);
-            *reinterpret_cast<f32x4*>(B + (lrow + 32) * kGL + col) = mask4<VEC>(v[4 * cs + 3], k, k_hi);
-        }
-    };
-    f32x16 acc2[2];
-#pragma unroll
-    for (int g = 0; g < 16; ++g) acc2[0][g] = acc2[1][g] = 0.f;
-    float sa = 0.f, sb = 0.f;
-    const int arow = (qd >> 1) * 32 + r, brow = (qd & 1) * 32 + r;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) gload(c, ring[c]);
-    // one super-chunk: chunks straight from the ring.  Several: ring slot c is reloaded with
-    // the next super-chunk's chunk c right after it went to LDS -- unconditionally (the last
-    // super-chunk re-reads its own, clamped), so the outstanding-load count is the same on
-    // every path and the compiler waits for exactly the slot it stores next.
-    auto run_super = [&](int sc, auto reload) {
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const int buf = (sc * NCH + c) & 1;
-            lstore(sc * NCH + c, buf, ring[c]);
-            if constexpr (decltype(reload)::value) gload(min(sc + 1, nsup - 1) * NCH + c, ring[c]);
-            __syncthreads();
-            if (sc == 0 && c == 0) GLL_TRACE_PT(15);
-            // wave half kh takes k [kh GK/2, (kh+1) GK/2) of the chunk, 32 at a time
-#pragma unroll
-            for (int sub = 0; sub < CS; ++sub) {
-                const int ko = kh * (GK / 2) + sub * 32 + 4 * h;
-                const float* A = smem + (buf * 2 + 0) * 64 * kGL + arow * kGL + ko;
-                const float* B = smem + (buf * 2 + 1) * 64 * kGL + brow * kGL + ko;
-                f32x4 a[4], b[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    a[u] = *reinterpret_cast<const f32x4*>(A + 8 * u);
-                    b[u] = *reinterpret_cast<const f32x4*>(B + 8 * u);
-                }
-                gram_chunk_mfma(a, b, acc2, sa, sb);
-            }
-        }
-    };
-    if (nsup == 1) {
-        run_super(0, std::false_type{});
-        GLL_TRACE_PT(11);
-    } else {
-        for (int sc = 0; sc < nsup; ++sc) run_super(sc, std::true_type{});
-    }
-    __syncthreads();
-    GLL_TRACE_PT(12);
-    f32x16 acc = acc2[0] + acc2[1];
-    // combine the k-halves in a fixed order (half 0 + half 1) through LDS
-    float* part = smem;                    // [4 quadrants][16][64]
-    float* nrm = smem + 4 * 16 * 64;       // [2][4][64]
-    if (kh == 1) {
-#pragma unroll
-        for (int g = 0; g < 16; ++g) part[(qd * 16 + g) * 64 + lane] = acc[g];
-        nrm[(0 * 4 + qd) * 64 + lane] = sa;
-        nrm[(1 * 4 + qd) * 64 + lane] = sb;
-    }
-    __syncthreads();
-    if (kh == 0) {
-#pragma unroll
-        for (int g = 0; g < 16; ++g) acc[g] += part[(qd * 16 + g) * 64 + lane];
-        sa += nrm[(0 * 4 + qd) * 64 + lane];
-        sb += nrm[(1 * 4 + qd) * 64 + lane];
-        sa += __shfl_xor(sa, 32);   // the two k quarters of row r
-        sb += __shfl_xor(sb, 32);
-        if (h == 0) {
-            if ((qd & 1) == 0) s_sq[0][(qd >> 1) * 32 + r] = sa;
-            if ((qd >> 1) == 0) s_sq[1][(qd & 1) * 32 + r] = sb;
-        }
-    }
-    __syncthreads();
-    float* tile = smem + 8 * 16 * 64;      // [64][65], past part/nrm
-    if (kh == 0) {
-        const int tc = (qd & 1) * 32 + r;
-        const float sqc = s_sq[1][tc];
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-            const int tr = (qd >> 1) * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
-            tile[tr * 65 + tc] = s_sq[0][tr] + sqc - 2.f * acc[g];
-        }
-    }
-    __syncthreads();
-    GLL_TRACE_PT(13);
-    float* P = D2 + size_t(ks) * plane;
-    const int cr = tid >> 4, cc = (tid & 15) * 4;
-    for (int rr = cr; rr < 64; rr += 32) {
-        const int i = bi * 64 + rr;
-        if (i < n) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (bj * 64 + cc + t < n) P[size_t(i) * ld + bj * 64 + cc + t] = tile[rr * 65 + cc + t];
-        }
-        const int jr = bj * 64 + rr;
-        if (bi != bj && jr < n) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (bi * 64 + cc + t < n) P[size_t(jr) * ld + bi * 64 + cc + t] = tile[(cc + t) * 65 + rr];
-        }
-    }
-    GLL_TRACE_PT(14);
-#ifdef GLL_TRACE
-    if (blockIdx.x == 0 && threadIdx.x == 0) g_trace[22] = __builtin_amdgcn_s_memtime();
-#endif
-}
-
-// --------------------------------------------------------------------------------------
-// K1a'': 48 x 48 tiles for small problems, where 64-tiles leave CUs idle (n = 1000: 136 64-tiles
-// vs 231 48-tiles for 256 CUs).  v_mfma_f32_16x16x4f32 (A[l&15][k=l>>4], B[k=l>>4][l&15];
-// C col = l&15, row = 4(l>>4) + reg).  12 waves = 4 k-quarters of each 64-deep chunk x 3
-// row blocks; a wave owns the 3 blocks of its row (3 independent accumulators).  Lane group
-// g = l >> 4 takes k = 16 kq + 4 g + s at step s, so one ds_read_b128 feeds 4 MFMA steps.
-// --------------------------------------------------------------------------------------
-constexpr int k48L = kGK + 4;   // padded LDS row (floats)
-
-template <bool VEC, int NCH>
-__global__ __launch_bounds__(768) void gram48_kernel(const float* __restrict__ X, int n, int d,
-                                                     int T, float* __restrict__ D2, int ld,
-                                                     int32_t* __restrict__ status,
-                                                     int32_t* __restrict__ rev_cnt,
-                                                     size_t xs, size_t wss) {
-    GLL_TRACE_SCOPE(3);
-    X = gshift_br(X, xs);
-    D2 = gshift_br(D2, wss);
-    status = gshift_br(status, wss);
-    rev_cnt = gshift_br(rev_cnt, wss);
-    // stage[buf][A|B][48][k48L]; the epilogue reuses it: partials [4][3][3][4][64], norms
-    // 2 x [4][3][64], tile [48][49] -- sized for the larger of the two
-    constexpr int kStage = 2 * 2 * 48 * k48L;
-    constexpr int kEpi = 4 * 3 * 3 * 256 + 2 * 4 * 3 * 64 + 48 * 49;
-    __shared__ __attribute__((aligned(16))) float smem[kStage > kEpi ? kStage : kEpi];
-    __shared__ float s_sq[2][48];
-    const int tid = threadIdx.x;
-    const int lane = lane_id();
-    const int wave = tid >> 6;
-    const int kq = wave / 3, rb = wave % 3;
-    const int lr = lane & 15, lg = lane >> 4;
-    int bi = 0, rem = blockIdx.x;
-    while (rem >= T - bi) {
-        rem -= T - bi;
-        ++bi;
-    }
-    const int bj = bi + rem;
-    {   // per-call reset of the counters the select kernel accumulates into
-        const int g = blockIdx.x * 768 + tid;
-        if (g < GLL_ST_NWORDS) status[g] = 0;
-        for (int q = g; q < n; q += gridDim.x * 768) rev_cnt[q] = 0;
-    }
-    // loader: thread t moves float4 column 4 (t & 15) of row t >> 4 (< 48) of A and of B
-    const int lrow = tid >> 4, lcol = 4 * (tid & 15);
-    const float* ga = X + size_t(min(bi * 48 + lrow, n - 1)) * d;
-    const float* gb = X + size_t(min(bj * 48 + lrow, n - 1)) * d;
-    const int nchunk = (d + kGK - 1) / kGK;
-    const int nsup = (nchunk + NCH - 1) / NCH;
-    f32x4 ring[NCH][2];
-    auto gload = [&](int chunk, f32x4 (&v)[2]) {
-        const int k = chunk * kGK + lcol;
-        v[0] = load4_raw<VEC>(ga, k, d);
-        v[1] = load4_raw<VEC>(gb, k, d);
-    };
-    auto lstore = [&](int chunk, int buf, const f32x4 (&v)[2]) {
-        const int k = chunk * kGK + lcol;
-        float* A = smem + (buf * 2 + 0) * 48 * k48L;
-        float* B = smem + (buf * 2 + 1) * 48 * k48L;
-        *reinterpret_cast<f32x4*>(A + lrow * k48L + lcol) = mask4<VEC>(v[0], k, d);
-        *reinterpret_cast<f32x4*>(B + lrow * k48L + lcol) = mask4<VEC>(v[1], k, d);
-    };
-    f32x4 acc[3];
-#pragma unroll
-    for (int cb = 0; cb < 3; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float sa = 0.f, sb[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) gload(min(c, nchunk - 1), ring[c]);
-    for (int sc = 0; sc < nsup; ++sc) {
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const int chunk = sc * NCH + c;
-            if (chunk >= nchunk) break;   // uniform
-            const int buf = chunk & 1;
-            lstore(chunk, buf, ring[c]);
-            gload(min(chunk + NCH, nchunk - 1), ring[c]);   // unconditional: static counts
-            __syncthreads();
-            const int ko = 16 * kq + 4 * lg;
-            const float* A = smem + (buf * 2 + 0) * 48 * k48L;
-            const float* B = smem + (buf * 2 + 1) * 48 * k48L;
-            const f32x4 a = *reinterpret_cast<const f32x4*>(A + (16 * rb + lr) * k48L + ko);
-            f32x4 b[3];
-#pragma unroll
-            for (int cb = 0; cb < 3; ++cb)
-                b[cb] = *reinterpret_cast<const f32x4*>(B + (16 * cb + lr) * k48L + ko);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-#pragma unroll
-                for (int cb = 0; cb < 3; ++cb)
-                    acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[cb][t], acc[cb], 0, 0, 0);
-            }
-            sa += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
-#pragma unroll
-            for (int cb = 0; cb < 3; ++cb)
-                sb[cb] += b[cb].x * b[cb].x + b[cb].y * b[cb].y + b[cb].z * b[cb].z + b[cb].w * b[cb].w;
-        }
-    }
-    __syncthreads();
-    // combine the k-quarters in a fixed order through LDS
-    float* part = smem;                     // [kq][rb][cb][4][64]
-    float* nA = smem + 4 * 3 * 3 * 256;     // [kq][rb][64]
-    float* nB = nA + 4 * 3 * 64;            // [kq][cb][64]   (rb == 0 waves)
-#pragma unroll
-    for (int cb = 0; cb < 3; ++cb)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) part[(((kq * 3 + rb) * 3 + cb) * 4 + g) * 64 + lane] = acc[cb][g];
-    nA[(kq * 3 + rb) * 64 + lane] = sa;
-    if (rb == 0) {
-#pragma unroll
-        for (int cb = 0; cb < 3; ++cb) nB[(kq * 3 + cb) * 64 + lane] = sb[cb];
-    }
-    __syncthreads();
-    if (tid < 96) {   // row norms: 48 A rows, 48 B rows; sum over k-quarters and lane groups
-        const int which = tid / 48, row = tid % 48, blk = row >> 4, r16 = row & 15;
-        const float* src = which == 0 ? nA : nB;
-        float s = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) s += src[(q * 3 + blk) * 64 + g * 16 + r16];
-        s_sq[which][row] = s;
-    }
-    __syncthreads();
-    float* tile = nB + 4 * 3 * 64;          // [48][49]
-    if (kq == 0) {
-#pragma unroll
-        for (int cb = 0; cb < 3; ++cb) {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                float v = 0.f;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) v += part[(((q * 3 + rb) * 3 + cb) * 4 + g) * 64 + lane];
-                const int tr = 16 * rb + 4 * lg + g, tc = 16 * cb + lr;
-                tile[tr * 49 + tc] = s_sq[0][tr] + s_sq[1][tc] - 2.f * v;
-            }
-        }
-    }
-    __syncthreads();
-    if (tid < 48 * 12) {   // 48 rows x 12 groups of 4 columns, both orientations
-        const int rr = tid / 12, cc = (tid % 12) * 4;
-        const int i = bi * 48 + rr;
-        if (i < n) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (bj * 48 + cc + t < n) D2[size_t(i) * ld + bj * 48 + cc + t] = tile[rr * 49 + cc + t];
-        }
-        const int jr = bj * 48 + rr;
-        if (bi != bj && jr < n) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (bi * 48 + cc + t < n) D2[size_t(jr) * ld + bi * 48 + cc + t] = tile[(cc + t) * 49 + rr];
-        }
-    }
-}
 
 // --------------------------------------------------------------------------------------
 // K1a (default): split-bf16 Gram on v_mfma_f32_32x32x16_bf16.  Each fp32 feature is split as
@@ -427,6 +70,7 @@ __device__ __forceinline__ int xcd_tile(int b, int nt) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int kBP = 256;            // features per phase
+constexpr int kMaxCen = 4096;       // LDS copy of the centre row: d <= 4096 (gll.h limit)
 constexpr int kBS = kBP + 8;        // LDS plane row stride (bf16)
 
 // Epilogue of the 64-tile split-bf16 Gram: row norms (wave sums of the per-slot squares),
@@ -541,6 +185,7 @@ __global__ __launch_bounds__(1024) void gram_bf3_kernel(const float* __restrict_
     __shared__ __attribute__((aligned(16))) __bf16 smem_h[2 * kPlane];
     __shared__ float sqp[8][16];                                        // [slot][wave]
     __shared__ float nrm[128];
+    __shared__ __attribute__((aligned(16))) float cen[kMaxCen];          // centre row x_0
     float* smem = reinterpret_cast<float*>(smem_h);
     const int tid = threadIdx.x;
     const int lane = lane_id();
@@ -580,10 +225,11 @@ __global__ __launch_bounds__(1024) void gram_bf3_kernel(const float* __restrict_
     };
     auto phase = [&](int ph, const f32x4 (&v)[8]) {
         const int k = ph * kBP + fo;
-        __syncthreads();   // the previous phase's fragment reads are done
+        __syncthreads();   // the previous phase's fragment reads are done (and cen is staged)
+        const f32x4 c = *reinterpret_cast<const f32x4*>(cen + ph * kBP + fo);
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-            const f32x4 f = mask4<VEC>(v[s], k, d);
+            const f32x4 f = mask4<VEC>(v[s] - c, k, d);
             sq[s] += f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
             bf16x4 hv, lv;
 #pragma unroll
@@ -611,8 +257,12 @@ __global__ __launch_bounds__(1024) void gram_bf3_kernel(const float* __restrict_
         }
     };
     {
+        // the centre row (row 0 of the graph) into LDS: issued first, so staging it waits for
+        // that load only (loads return in order) while the first phase's rows stay in flight
+        const f32x4 cv = load4_raw<VEC>(X, 4 * tid, d);
         f32x4 va[8], vb[8];
         gload(0, va);
+        if (4 * tid < nph * kBP) *reinterpret_cast<f32x4*>(cen + 4 * tid) = mask4<VEC>(cv, 4 * tid, d);
         for (int ph = 0; ph < nph; ph += 2) {
             gload(ph + 1 < nph ? ph + 1 : ph, vb);   // unconditional: static vmcnt counts
 #ifdef GLL_TRACE
@@ -691,11 +341,14 @@ __global__ __launch_bounds__(1024) void gram_bf3s_kernel(const float* __restrict
         const int k = (dg ? (s >> 2) : half) * kBP + fo;
         v[s] = load4_raw<VEC>(X + size_t(row < n ? row : n - 1) * d, k, d);
     }
+    // centre row (row 0 of the graph) over the phase(s) this workgroup multiplies
+    const f32x4 cen0 = load4_raw<VEC>(X, (dg ? 0 : half) * kBP + fo, d);
+    const f32x4 cen1 = load4_raw<VEC>(X, (dg ? 1 : half) * kBP + fo, d);
     float sq[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
         const int k = (dg ? (s >> 2) : half) * kBP + fo;
-        const f32x4 f = mask4<VEC>(v[s], k, d);
+        const f32x4 f = mask4<VEC>(v[s] - (s >= 4 ? cen1 : cen0), k, d);
         sq[s] = f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
         bf16x4 hv, lv;
 #pragma unroll
@@ -773,6 +426,7 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
     constexpr int kPlane = 256 * kWS;                                   // bf16 per plane
     __shared__ __attribute__((aligned(16))) __bf16 smem_h[2 * kPlane];  // 136 KiB
     __shared__ float nrm[256];
+    __shared__ __attribute__((aligned(16))) float cen[kMaxCen];          // centre row x_0
     float* smem = reinterpret_cast<float*>(smem_h);
     const int tid = threadIdx.x;
     const int lane = lane_id();
@@ -811,10 +465,11 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
     };
     auto phase = [&](int ph, const f32x4 (&v)[8]) {
         const int k = ph * kWP + fo;
-        __syncthreads();   // the previous phase's fragment reads are done
+        __syncthreads();   // the previous phase's fragment reads are done (and cen is staged)
+        const f32x4 c = *reinterpret_cast<const f32x4*>(cen + ph * kWP + fo);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            const f32x4 f = mask4<VEC>(v[q], k, d);
+            const f32x4 f = mask4<VEC>(v[q] - c, k, d);
             float t = f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
             t = dpp_add<0xB1, 0xf>(t);    // quad
             t = dpp_add<0x4E, 0xf>(t);
@@ -848,8 +503,10 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
         }
     };
     {
+        const f32x4 cv = load4_raw<VEC>(X, 4 * tid, d);   // centre row x_0 -> LDS (see gram_bf3)
         f32x4 va[8], vb[8];
         gload(0, va);
+        if (4 * tid < nph * kWP) *reinterpret_cast<f32x4*>(cen + 4 * tid) = mask4<VEC>(cv, 4 * tid, d);
         for (int ph = 0; ph < nph; ph += 2) {
             gload(ph + 1 < nph ? ph + 1 : ph, vb);   // unconditional: static vmcnt counts
             phase(ph, va);
@@ -905,170 +562,6 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
             const int ti = q >> 7, tj = q & 127;
             const int i = bi * 128 + ti, j = bi * 128 + tj;
             if (i < n && j < n) D2[size_t(i) * ld + j] = tj >= ti ? tile[ti * 129 + tj] : tile[tj * 129 + ti];
-        }
-    }
-}
-
-// --------------------------------------------------------------------------------------
-// K1a': wide symmetric Gram tile for large problems (many tiles): 128 x 128 per workgroup, 4
-// waves each owning a 64 x 64 sub-tile as 2 x 2 independent 32 x 32 MFMA accumulators (one
-// A fragment feeds two MFMAs, four chains keep the MFMA pipe full from one wave per SIMD),
-// 32-deep chunks through a register ring of NCH chunks into double-buffered LDS.
-// --------------------------------------------------------------------------------------
-constexpr int kWK = 32;           // k per chunk
-constexpr int kWL = kWK + 4;      // padded LDS row (floats)
-
-template <bool VEC, int NCH>
-__global__ __launch_bounds__(256) void gram_wide_kernel(const float* __restrict__ X, int n, int d,
-                                                        int T, float* __restrict__ D2, int ld,
-                                                        int32_t* __restrict__ status,
-                                                        int32_t* __restrict__ rev_cnt,
-                                                        size_t xs, size_t wss) {
-    GLL_TRACE_SCOPE(2);
-    X = gshift_br(X, xs);
-    D2 = gshift_br(D2, wss);
-    status = gshift_br(status, wss);
-    rev_cnt = gshift_br(rev_cnt, wss);
-    // stage[buf][A|B][128][kWL]; the epilogue reuses it as tile[128][129]
-    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * 128 * kWL];
-    __shared__ float s_sq[2][128];
-    const int tid = threadIdx.x;
-    const int lane = lane_id();
-    const int wave = tid >> 6;
-    const int wr = wave >> 1, wc = wave & 1;   // 64-row / 64-column half of the tile
-    const int r = lane & 31, h = lane >> 5;
-    int bi = 0, rem = blockIdx.x;
-    while (rem >= T - bi) {
-        rem -= T - bi;
-        ++bi;
-    }
-    const int bj = bi + rem;
-    {   // per-call reset of the counters the select kernel accumulates into
-        const int g = blockIdx.x * 256 + tid;
-        if (g < GLL_ST_NWORDS) status[g] = 0;
-        for (int q = g; q < n; q += gridDim.x * 256) rev_cnt[q] = 0;
-    }
-    // loader: thread t moves float4 column 4 (t & 7) of rows (t >> 3) + 32 s, s < 4, of A and B
-    const int lrow = tid >> 3, lcol = 4 * (tid & 7);
-    const float* ga[4];
-    const float* gb[4];
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-        ga[s4] = X + size_t(min(bi * 128 + lrow + 32 * s4, n - 1)) * d;
-        gb[s4] = X + size_t(min(bj * 128 + lrow + 32 * s4, n - 1)) * d;
-    }
-    const int nchunk = (d + kWK - 1) / kWK;
-    const int nsup = (nchunk + NCH - 1) / NCH;
-    f32x4 ring[NCH][8];
-    auto gload = [&](int chunk, f32x4 (&v)[8]) {   // raw: masked when stored to LDS
-        const int k = chunk * kWK + lcol;
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-            v[s4] = load4_raw<VEC>(ga[s4], k, d);
-            v[4 + s4] = load4_raw<VEC>(gb[s4], k, d);
-        }
-    };
-    auto lstore = [&](int chunk, int buf, const f32x4 (&v)[8]) {
-        const int k = chunk * kWK + lcol;
-        float* A = smem + (buf * 2 + 0) * 128 * kWL;
-        float* B = smem + (buf * 2 + 1) * 128 * kWL;
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-            *reinterpret_cast<f32x4*>(A + (lrow + 32 * s4) * kWL + lcol) = mask4<VEC>(v[s4], k, d);
-            *reinterpret_cast<f32x4*>(B + (lrow + 32 * s4) * kWL + lcol) = mask4<VEC>(v[4 + s4], k, d);
-        }
-    };
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.f;
-    float sa[2] = {0.f, 0.f}, sb[2] = {0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) gload(min(c, nchunk - 1), ring[c]);
-    for (int sc = 0; sc < nsup; ++sc) {
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const int chunk = sc * NCH + c;
-            if (chunk >= nchunk) break;   // uniform
-            const int buf = chunk & 1;
-            lstore(chunk, buf, ring[c]);
-            gload(min(chunk + NCH, nchunk - 1), ring[c]);   // unconditional: static counts
-            __syncthreads();
-            const float* A = smem + (buf * 2 + 0) * 128 * kWL;
-            const float* B = smem + (buf * 2 + 1) * 128 * kWL;
-            f32x4 a[2][4], b[2][4];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    a[i][u] = *reinterpret_cast<const f32x4*>(A + (64 * wr + 32 * i + r) * kWL + 4 * h + 8 * u);
-                    b[i][u] = *reinterpret_cast<const f32x4*>(B + (64 * wc + 32 * i + r) * kWL + 4 * h + 8 * u);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-#pragma unroll
-                    for (int i = 0; i < 2; ++i)
-#pragma unroll
-                        for (int j = 0; j < 2; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][u][t], b[j][u][t],
-                                                                           acc[i][j], 0, 0, 0);
-                }
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    sa[i] += a[i][u].x * a[i][u].x + a[i][u].y * a[i][u].y +
-                             a[i][u].z * a[i][u].z + a[i][u].w * a[i][u].w;
-                    sb[i] += b[i][u].x * b[i][u].x + b[i][u].y * b[i][u].y +
-                             b[i][u].z * b[i][u].z + b[i][u].w * b[i][u].w;
-                }
-            }
-        }
-    }
-    __syncthreads();   // (one barrier per chunk suffices: buffer `buf` is rewritten only after
-                       //  every wave has passed the next chunk's barrier)
-    // row norms: the two k-quarters of a lane pair (xor 32), A rows from wc == 0 waves, B rows
-    // (columns) from wr == 0 waves
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        sa[i] += __shfl_xor(sa[i], 32);
-        sb[i] += __shfl_xor(sb[i], 32);
-        if (h == 0 && wc == 0) s_sq[0][64 * wr + 32 * i + r] = sa[i];
-        if (h == 0 && wr == 0) s_sq[1][64 * wc + 32 * i + r] = sb[i];
-    }
-    __syncthreads();
-    float* tile = smem;   // [128][129]
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int tc = 64 * wc + 32 * j + r;
-            const float sqc = s_sq[1][tc];
-#pragma unroll
-            for (int g = 0; g < 16; ++g) {
-                const int tr = 64 * wr + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
-                tile[tr * 129 + tc] = s_sq[0][tr] + sqc - 2.f * acc[i][j][g];
-            }
-        }
-    }
-    __syncthreads();
-    const int cr = tid >> 5, cc = (tid & 31) * 4;
-    for (int rr = cr; rr < 128; rr += 8) {
-        const int i = bi * 128 + rr;
-        if (i < n) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (bj * 128 + cc + t < n) D2[size_t(i) * ld + bj * 128 + cc + t] = tile[rr * 129 + cc + t];
-        }
-        const int jr = bj * 128 + rr;
-        if (bi != bj && jr < n) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (bi * 128 + cc + t < n) D2[size_t(jr) * ld + bi * 128 + cc + t] = tile[(cc + t) * 129 + rr];
         }
     }
 }
@@ -1176,13 +669,17 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 }
 
 // Exact merge (fallback): round t hands the t-th smallest (d2, index) key to lane t.
+// `tb` receives the D2 bits of the kc-th key (every column left out is >= it), or +inf when
+// fewer than kc valid columns exist (then every one of them is a candidate).
 template <int KC>
-__device__ __forceinline__ int merge_exact(uint64_t (&key)[KC], int kc) {
+__device__ __forceinline__ int merge_exact(uint64_t (&key)[KC], int kc, uint32_t& tb) {
     const int lane = lane_id();
     uint64_t mine = ~0ull;
+    tb = 0x7F800000u;
     for (int t = 0; t < kc; ++t) {
         const uint64_t best = wave_min_u64(key[0]);
         if (lane == t) mine = best;
+        if (best != ~0ull && t == kc - 1) tb = uint32_t(best >> 32);
         list_pop<KC>(key, best != ~0ull && key[0] == best);
     }
     return mine == ~0ull ? -1 : int(uint32_t(mine));
@@ -1220,7 +717,8 @@ __device__ __forceinline__ bool merge_fast(uint64_t (&key)[KS], int kc, int seen
 // candidates tie in; the caller then re-runs the exact merge.
 template <int KS>
 __device__ __forceinline__ bool merge_threshold(const uint64_t (&key)[KS], int kc, int seen,
-                                                int* __restrict__ cand, int& ci, int& kce) {
+                                                int* __restrict__ cand, int& ci, int& kce,
+                                                uint32_t& tb) {
     const int lane = lane_id();
     uint32_t hv[KS];
 #pragma unroll
@@ -1237,14 +735,16 @@ __device__ __forceinline__ bool merge_threshold(const uint64_t (&key)[KS], int k
     const uint32_t hmax = wave_max_u32(hv[0] == 0xFFFFFFFFu ? 0u : hv[0]);
     if (lo > up) lo = up;   // every list empty
     if (hmax >= lo && count_le(hmax) >= kc) up = hmax;
+    tb = 0x7F800000u;        // fewer than kc valid entries: all of them are candidates
     if (count_le(up) >= kc) {
         while (lo < up) {   // smallest T with count_le(T) >= kc (wave-uniform, <= 32 steps)
             const uint32_t mid = lo + ((up - lo) >> 1);
             if (count_le(mid) >= kc) up = mid;
             else lo = mid + 1u;
         }
+        tb = up;             // the kc-th smallest D2: every column left out is > it
     }
-    const uint32_t T = up;   // fewer than kc valid entries: all of them
+    const uint32_t T = up;
     const uint64_t below = (1ull << lane) - 1ull;
     int mine = 0, before = 0, total = 0;
 #pragma unroll
@@ -1266,6 +766,117 @@ __device__ __forceinline__ bool merge_threshold(const uint64_t (&key)[KS], int k
     ci = (!redo && lane < total) ? cand[lane] : -1;
     return redo;
 }
+
+// 64-bit DPP add of the 8-lane group butterfly (two 32-bit moves per stage).
+template <int CTRL>
+__device__ __forceinline__ double dpp_add_d(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0, uint32_t(b), CTRL, 0xf, 0xf, false);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0, uint32_t(b >> 32), CTRL, 0xf, 0xf, false);
+    return v + __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+__device__ __forceinline__ double group8_sum_d(double v) {
+    v = dpp_add_d<0xB1>(v);
+    v = dpp_add_d<0x4E>(v);
+    v = dpp_add_d<0x141>(v);
+    return v;
+}
+__device__ __forceinline__ double shfl_d(double v, int src) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = uint32_t(__shfl(int(uint32_t(b)), src));
+    const uint32_t hi = uint32_t(__shfl(int(uint32_t(b >> 32)), src));
+    return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(b), l);
+    const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(b >> 32), l);
+    return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+
+// Exact squared distances d(i, c_L)^2 for the candidates c_L held by lanes L in [lo, hi)
+// (ci = -1: no candidate), 8 lanes per candidate across d, PG groups of 8 candidates per
+// sweep with every load in flight.  The differences and the sum are float64 -- the
+// reference's stand-in ranks in float64 -- so the order agrees with it
+// except at relative gaps ~1e-15, and the (i, j) and (j, i) sums run the same lane mapping
+// on negated differences: bitwise symmetric.  Lanes outside [lo, hi) keep `ce`.
+template <bool VEC, int PG>
+__device__ __forceinline__ double exact_d2(const float* __restrict__ X, const float* __restrict__ xi,
+                                           int i, int d, int ci, int lo, int hi, double ce) {
+    const int lane = lane_id();
+    const int grp = lane >> 3, sub = lane & 7;
+    for (int p0 = lo; p0 < hi; p0 += 8 * PG) {
+        const float* xj[PG];
+#pragma unroll
+        for (int g2 = 0; g2 < PG; ++g2) {
+            const int idx = p0 + 8 * g2 + grp;
+            const int j = __shfl(ci, idx < hi ? idx : lo);
+            const bool live = idx < hi && j >= 0;
+            xj[g2] = X + size_t(live ? j : i) * d;
+        }
+        double part[PG];
+#pragma unroll
+        for (int g2 = 0; g2 < PG; ++g2) part[g2] = 0.0;
+        for (int kb = 0; kb < d; kb += 512) {   // 16 steps of 32 features: all loads in flight
+            f32x4 va[16], vb[PG][16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {   // straight-line: every load issued before use
+                const int k = kb + 32 * u + 4 * sub;
+                va[u] = load4_raw<VEC>(xi, k, d);
+#pragma unroll
+                for (int g2 = 0; g2 < PG; ++g2) vb[g2][u] = load4_raw<VEC>(xj[g2], k, d);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {   // same order from either end: symmetric in (i, j)
+                const int k = kb + 32 * u + 4 * sub;
+                const f32x4 a = mask4<VEC>(va[u], k, d);
+                const double a0 = a.x, a1 = a.y, a2 = a.z, a3 = a.w;
+#pragma unroll
+                for (int g2 = 0; g2 < PG; ++g2) {
+                    const f32x4 b = mask4<VEC>(vb[g2][u], k, d);
+                    const double d0 = a0 - double(b.x), d1 = a1 - double(b.y);
+                    const double d2 = a2 - double(b.z), d3 = a3 - double(b.w);
+                    part[g2] = __builtin_fma(d0, d0, part[g2]);
+                    part[g2] = __builtin_fma(d1, d1, part[g2]);
+                    part[g2] = __builtin_fma(d2, d2, part[g2]);
+                    part[g2] = __builtin_fma(d3, d3, part[g2]);
+                }
+            }
+        }
+#pragma unroll
+        for (int g2 = 0; g2 < PG; ++g2) {
+            const double tot = group8_sum_d(part[g2]);
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const double v = readlane_d(tot, 8 * g);
+                if (lane == p0 + 8 * g2 + g) ce = v;
+            }
+        }
+    }
+    return ce;
+}
+
+// Rank of this lane's (exact d^2, index) key among lanes [0, cnt); lanes without a candidate
+// (ci < 0) sort last.
+__device__ __forceinline__ int key_rank(double ce, int ci, int cnt) {
+    const int me = ci < 0 ? INT_MAX : ci;
+    int rank = 0;
+    for (int u = 0; u < cnt; ++u) {
+        const double du = readlane_d(ce, u);
+        const int iu0 = __builtin_amdgcn_readlane(ci, u);
+        const int iu = iu0 < 0 ? INT_MAX : iu0;
+        rank += (du < ce || (du == ce && iu < me)) ? 1 : 0;
+    }
+    return rank;
+}
+
+// Conservative bound on |D2_gram(i, j) - d(i, j)^2| for the split-bf16 Gram over centred rows
+// a = x - x_0: the dropped lo*lo terms and the bf16 rounding of lo (<= 3 * 2^-18 |a_k b_k|,
+// doubled by the -2<a, b> term: 2^-15.4 |a||b|), plus fp32 accumulation at the kernels'
+// depth (<= 3d/16 MFMA steps: 2^-24 * 3d/16 * 2 |a||b|, 1.1e-5 |a||b| at d = 1024) and the
+// rounding of the centring and of the norms -- all below 2^-13 (|a| + |b|)^2 >= 2^-11 |a||b|
+// for d <= 8192 (gll.h caps d at 4096).
+constexpr double kGramErr = 1.0 / 8192.0;
 
 template <int KC, bool VEC, int NP, int PG>
 __global__ __launch_bounds__(256) void knn_select_kernel(
@@ -1290,102 +901,124 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     status_pub = gshift(status_pub, sts);
     __shared__ int s_cand[4][kWave];
     const int lane = lane_id();
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int wv = threadIdx.x >> 6;
+    const int i = blockIdx.x * 4 + wv;
     if (i >= n) return;  // whole wave
 
-    // 1-2) candidates: short per-lane lists + threshold merge, exact re-run when inexact
+    // 1-2) candidates: short per-lane lists + threshold merge, exact re-run when inexact.
+    //      tb: D2 bits every non-candidate column is >= to (+inf: all valid columns taken)
     const float* row = D2 + size_t(i) * ld;
     constexpr int KS = KC <= 16 ? 4 : 8;
     int ci, kce;
+    uint32_t tb;
     {
         uint64_t key[KS];
         const int seen = scan_row<KS, NP>(row, plane, n, ld, i, key);
         GLL_TRACE_PT(16);
-        const bool redo = merge_threshold<KS>(key, kc, seen, s_cand[threadIdx.x >> 6], ci, kce);
+        const bool redo = merge_threshold<KS>(key, kc, seen, s_cand[wv], ci, kce, tb);
         GLL_TRACE_PT(17);
         if (redo) {
             uint64_t full[KC];
             scan_row<KC, NP>(row, plane, n, ld, i, full);
-            ci = merge_exact<KC>(full, kc);
+            ci = merge_exact<KC>(full, kc, tb);
             kce = kc;
         }
     }
-    // 3) exact squared distances, 8 candidates per pass (8 lanes each, across d).  PG passes
-    //    per sweep with every load in flight at once: PG = 2 for single-graph launches (one
-    //    wave per SIMD anyway); batches keep PG = 1 (191 VGPRs at PG = 2 cost them 20-45%
-    //    occupancy).  Per-candidate arithmetic is the same either way.
-    const int grp = lane >> 3, sub = lane & 7;
+    // 3) exact float64 squared distances of the candidates.  PG passes per sweep for single
+    //    graphs (one wave per SIMD anyway); batches keep PG = 1 (register pressure).
     const float* xi = X + size_t(i) * d;
-    float ce = __builtin_inff();
-    for (int p0 = 0; p0 < kce; p0 += 8 * PG) {
-        const float* xj[PG];
+    double ce = exact_d2<VEC, PG>(X, xi, i, d, ci, 0, kce, __builtin_inf());
+    GLL_TRACE_PT(18);
+    if (ci < 0) ce = __builtin_inf();
+    // 4) rank the candidates by (exact d^2, index); keep the K-1 nearest
+    int rank = key_rank(ce, ci, kce);
+    bool keep = lane < kce && ci >= 0 && rank < K - 1;
+    int nkeep = __popcll(__ballot(keep));
+
+    // 5) certificate: every column left out has D2_gram >= tb; a left-out j that belongs in
+    //    the K-1 nearest has d_ij^2 <= dK (the (K-1)-th exact distance found) and so
+    //    |a_j| <= |a_i| + sqrt(dK), D2_gram <= dK + B with B = kGramErr (2|a_i| + sqrt(dK))^2.
+    //    tb > dK + B rules that out.  |a_i|^2 = D2[i][0] (row 0 is the Gram's centre, a_0 = 0).
+    //    Otherwise (rare: features far from row 0 relative to the neighbour gaps) every
+    //    column with D2_gram <= dK + B is re-ranked exactly, K-1 best kept across chunks.
+    if (K >= 2 && nkeep == K - 1 && tb < 0x7F800000u) {
+        const uint64_t kb = __ballot(keep && rank == K - 2);
+        const double dK = readlane_d(ce, int(__builtin_ctzll(kb)));
+        float a2 = row[0];
 #pragma unroll
-        for (int g2 = 0; g2 < PG; ++g2) {
-            const int idx = p0 + 8 * g2 + grp;
-            const int j = __shfl(ci, idx < kce ? idx : 0);
-            const bool live = idx < kce && j >= 0;
-            xj[g2] = X + size_t(live ? j : i) * d;
-        }
-        float part[PG];
+        for (int p = 1; p < NP; ++p) a2 += row[p * plane];
+        const double ai = sqrt(double(a2 > 0.f ? a2 : 0.f));
+        const double r = 2.0 * ai + sqrt(dK);
+        const double thr = dK + kGramErr * r * r;
+        if (!(double(__uint_as_float(tb)) > thr)) {
+            if (lane == 0) atomicAdd(&status_pub[GLL_ST_KNN_RESCAN], 1);
+            const int F = kWave - (K - 1);          // free lanes per chunk (launch: K-1 <= 56)
+            int bi = -1;                             // running best: lanes 0..K-2
+            double bd = __builtin_inf();
+            for (int jb = 0; jb < n; jb += kWave) {
+                const int j = jb + lane;
+                float v = 0.f;
+                if (j < n) {
+                    v = row[j];
 #pragma unroll
-        for (int g2 = 0; g2 < PG; ++g2) part[g2] = 0.f;
-        for (int kb = 0; kb < d; kb += 512) {   // 16 steps of 32 features: all loads in flight
-            f32x4 va[16], vb[PG][16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {   // straight-line: every load issued before use
-                const int k = kb + 32 * u + 4 * sub;
-                va[u] = load4_raw<VEC>(xi, k, d);
-#pragma unroll
-                for (int g2 = 0; g2 < PG; ++g2) vb[g2][u] = load4_raw<VEC>(xj[g2], k, d);
-            }
-#pragma unroll
-            for (int g2 = 0; g2 < PG; ++g2) {
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {   // same order from either end: symmetric in (i, j)
-                    const int k = kb + 32 * u + 4 * sub;
-                    const f32x4 df = mask4<VEC>(va[u] - vb[g2][u], k, d);
-                    part[g2] += df.x * df.x;
-                    part[g2] += df.y * df.y;
-                    part[g2] += df.z * df.z;
-                    part[g2] += df.w * df.w;
+                    for (int p = 1; p < NP; ++p) v += row[p * plane + j];
+                }
+                bool take = j < n && j != i && v == v && double(v) <= thr;
+                uint64_t mask = __ballot(take);
+                while (mask) {
+                    const int pos = lanes_below(mask);
+                    const bool sel = take && pos < F;
+                    if (sel) s_cand[wv][pos] = j;
+                    const int cnt = __popcll(__ballot(sel));
+                    mask &= ~__ballot(sel);
+                    take = take && !sel;
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+                    const int off = lane - (K - 1);
+                    int cc = lane < K - 1 ? bi : (off < cnt ? s_cand[wv][off] : -1);
+                    double cd = lane < K - 1 ? bd : __builtin_inf();
+                    cd = exact_d2<VEC, 1>(X, xi, i, d, cc, K - 1, K - 1 + cnt, cd);
+                    if (cc < 0) cd = __builtin_inf();
+                    const int rk = key_rank(cd, cc, K - 1 + cnt);
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+                    // keep the K-1 best in rank order: indices through LDS, distances by
+                    // readlane of the lane that holds rank L
+                    const uint64_t live = __ballot(lane < K - 1 + cnt && rk < K - 1 && cc >= 0);
+                    if (((live >> lane) & 1ull) != 0) s_cand[wv][rk] = lane;
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+                    const int nl = __popcll(live);
+                    const int src = lane < nl ? s_cand[wv][lane] : lane;
+                    const int nbi = __shfl(cc, src);
+                    const double nbd = shfl_d(cd, src);
+                    bi = lane < nl ? nbi : -1;
+                    bd = lane < nl ? nbd : __builtin_inf();
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
                 }
             }
-        }
-#pragma unroll
-        for (int g2 = 0; g2 < PG; ++g2) {
-            const float tot = group8_sum(part[g2]);
-#pragma unroll
-            for (int g = 0; g < 8; ++g) {
-                const float v = readlane_f(tot, 8 * g);
-                if (lane == p0 + 8 * g2 + g) ce = v;
-            }
+            ci = bi;
+            ce = bd;
+            kce = K - 1;
+            rank = key_rank(ce, ci, kce);
+            keep = lane < kce && ci >= 0 && rank < K - 1;
+            nkeep = __popcll(__ballot(keep));
         }
     }
-    GLL_TRACE_PT(18);
-    if (ci < 0) ce = __builtin_inff();
-    // 4) rank the candidates by (exact d^2, index); keep the K-1 nearest
-    const uint64_t myk = ci < 0 ? ~0ull : pack_key(ce, ci);
-    int rank = 0;
-    for (int u = 0; u < kce; ++u) {
-        const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(myk), u);
-        const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(myk >> 32), u);
-        const uint64_t ku = (uint64_t(hi) << 32) | lo;
-        rank += ku < myk ? 1 : 0;
-    }
-    const bool keep = lane < kce && ci >= 0 && rank < K - 1;
     int32_t* oi = knn_idx + size_t(i) * K;
     float* od = knn_d2 + size_t(i) * K;
+    const float cef = float(ce);   // correctly rounded exact d^2
     if (lane == 0) {
         oi[0] = i;
         od[0] = 0.f;
     }
     if (keep) {
         oi[1 + rank] = ci;
-        od[1 + rank] = ce;
+        od[1 + rank] = cef;
     }
     // rows with fewer valid candidates (non-finite input) fall back to self at distance 0,
     // i.e. dropped edges (sparse.find drops zeros, GLL.py:198)
-    const int nkeep = __popcll(__ballot(keep));
     if (lane >= nkeep && lane < K - 1) {
         oi[1 + lane] = i;
         od[1 + lane] = 0.f;
@@ -1394,7 +1027,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     float ei = eps_fixed;
     if (auto_eps) {
         // eps_i = d(i, knn_ind[i, K-1])  (GLL.py:205)
-        const float e = (keep && rank == K - 2) ? sqrtf(ce) : 0.f;
+        const float e = (keep && rank == K - 2) ? sqrtf(cef) : 0.f;
         ei = wave_sum_dpp(e);
     }
     if (lane == 0) {
@@ -1402,45 +1035,29 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
         if (!(ei >= 1e-10f)) atomicOr(&status_pub[GLL_ST_TINY_EPS], 1);  // GLL.py:240-241
     }
     // 5) reverse entry (ci, i) for every valid pair; zero distances never enter the graph
-    if (keep && ce > 0.f) {
+    if (keep && cef > 0.f) {
         const int pos = atomicAdd(&rev_cnt[ci], 1);
         if (pos < RCAP) {
             rev_idx[size_t(ci) * RCAP + pos] = i;
-            rev_d2[size_t(ci) * RCAP + pos] = ce;
+            rev_d2[size_t(ci) * RCAP + pos] = cef;
         } else {
             const int q = atomicAdd(&status[kStOvfCount], 1);
             ovf[3 * q + 0] = ci;
             ovf[3 * q + 1] = i;
-            ovf[3 * q + 2] = __float_as_int(ce);
+            ovf[3 * q + 2] = __float_as_int(cef);
         }
     }
 }
 
-// Wide 128-tiles when there are enough of them to fill the chip twice over (large graphs and
-// batches); the 64-tile kernel otherwise (a single NS graph has only 36 wide tiles).
-static bool use_wide_gram(const Layout& L, const Batch& bt) {
-    if (gram_planes(L, bt.B) != 1 || (L.flags & GLL_FLAG_GRAM_NARROW)) return false;
-    const int64_t T = (L.n + 127) / 128;
-    return int64_t(bt.B) * T * (T + 1) / 2 >= 512;
-}
-
-// 48-tiles when 64-tiles would leave a quarter of the CUs idle and 48-tiles fit in one round.
-static bool use_gram48(const Layout& L, const Batch& bt) {
-    if (gram_planes(L, bt.B) != 1 || (L.flags & GLL_FLAG_GRAM_NARROW)) return false;
-    const int64_t T64 = (L.n + 63) / 64, T48 = (L.n + 47) / 48;
-    return int64_t(bt.B) * T64 * (T64 + 1) / 2 < 192 && int64_t(bt.B) * T48 * (T48 + 1) / 2 <= 256;
-}
-
 hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
                        hipStream_t s) {
-    const int planes = gram_planes(L, bt.B);
-    if (planes == 2) {
+    float* D2 = L.at<float>(ws, L.D2);
+    int32_t* st = L.at<int32_t>(ws, L.status);
+    int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
+    if (gram_planes(L, bt.B) == 2) {
         const int T = (L.n + 63) / 64;
         const dim3 grid(T * T, bt.B);
-        float* D2 = L.at<float>(ws, L.D2);
         const size_t plane = size_t(L.n) * L.ldD;
-        int32_t* st = L.at<int32_t>(ws, L.status);
-        int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
         prof_begin(GLL_K_GRAM, s);
         if (vec)
             launch_k(gram_bf3s_kernel<true>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, plane, st, rc, bt.x, bt.ws);
@@ -1449,96 +1066,28 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         prof_end(GLL_K_GRAM, s);
         return launch_status("knn.hip:launch_gram(bf3s)");
     }
-    if (!(L.flags & GLL_FLAG_GRAM_F32) && !(L.flags & GLL_FLAG_GRAM_NARROW)) {
-        const int T = (L.n + 127) / 128;
-        if (int64_t(bt.B) * T * (T + 1) / 2 >= 512) {   // enough 128-tiles to fill the chip twice
-            const dim3 grid(T * (T + 1) / 2, bt.B);
-            float* D2 = L.at<float>(ws, L.D2);
-            int32_t* st = L.at<int32_t>(ws, L.status);
-            int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
-            prof_begin(GLL_K_GRAM, s);
-            if (vec)
-                launch_k(gram_bf3w_kernel<true>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
-            else
-                launch_k(gram_bf3w_kernel<false>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
-            prof_end(GLL_K_GRAM, s);
-            return launch_status("knn.hip:launch_gram(bf3w)");
-        }
-    }
-    if (!(L.flags & GLL_FLAG_GRAM_F32)) {
-        const int T = (L.n + 63) / 64;
+    // 128-tiles when there are enough of them to fill the chip twice (large graphs and batches;
+    // a single NS graph has only 36); 64-tiles otherwise
+    const int T = (L.n + 127) / 128;
+    if (!(L.flags & GLL_FLAG_GRAM_NARROW) && int64_t(bt.B) * T * (T + 1) / 2 >= 512) {
         const dim3 grid(T * (T + 1) / 2, bt.B);
-        float* D2 = L.at<float>(ws, L.D2);
-        int32_t* st = L.at<int32_t>(ws, L.status);
-        int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
         prof_begin(GLL_K_GRAM, s);
         if (vec)
-            launch_k(gram_bf3_kernel<true>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
+            launch_k(gram_bf3w_kernel<true>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
         else
-            launch_k(gram_bf3_kernel<false>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
+            launch_k(gram_bf3w_kernel<false>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
         prof_end(GLL_K_GRAM, s);
-        return launch_status("knn.hip:launch_gram(bf3)");
+        return launch_status("knn.hip:launch_gram(bf3w)");
     }
-    if (use_gram48(L, bt)) {
-        const int T = (L.n + 47) / 48;
-        const dim3 grid(T * (T + 1) / 2, bt.B);
-        float* D2 = L.at<float>(ws, L.D2);
-        int32_t* st = L.at<int32_t>(ws, L.status);
-        int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
-        const int nchunk = (L.d + kGK - 1) / kGK;
-        prof_begin(GLL_K_GRAM, s);
-#define GLL_G48(V, N) \
-    launch_k(gram48_kernel<V, N>, grid, 768, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws)
-        if (vec) { if (nchunk >= 4) GLL_G48(true, 4); else if (nchunk >= 2) GLL_G48(true, 2); else GLL_G48(true, 1); }
-        else { if (nchunk >= 4) GLL_G48(false, 4); else if (nchunk >= 2) GLL_G48(false, 2); else GLL_G48(false, 1); }
-#undef GLL_G48
-        prof_end(GLL_K_GRAM, s);
-        return launch_status("knn.hip:launch_gram(48)");
-    }
-    if (use_wide_gram(L, bt)) {
-        const int T = (L.n + 127) / 128;
-        const dim3 grid(T * (T + 1) / 2, bt.B);
-        float* D2 = L.at<float>(ws, L.D2);
-        int32_t* st = L.at<int32_t>(ws, L.status);
-        int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
-        const int nchunk = (L.d + kWK - 1) / kWK;
-        prof_begin(GLL_K_GRAM, s);
-#define GLL_WIDE(V, N) \
-    launch_k(gram_wide_kernel<V, N>, grid, 256, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws)
-        if (vec) { if (nchunk >= 2) GLL_WIDE(true, 2); else GLL_WIDE(true, 1); }
-        else { if (nchunk >= 2) GLL_WIDE(false, 2); else GLL_WIDE(false, 1); }
-#undef GLL_WIDE
-        prof_end(GLL_K_GRAM, s);
-        return launch_status("knn.hip:launch_gram(wide)");
-    }
-    const int T = (L.n + 63) / 64;
-    const int tiles = T * (T + 1) / 2;
-    const int KS = planes;
-    // slice of the features per split in whole 64-deep chunks, grouped NCH per super-chunk.
-    // (128-deep chunks -- half the barriers -- measured no faster at NS, B = 64 or stress:
-    // profiles/r01_gram_chunk_depth.txt; the template keeps the depth a parameter.)
-    constexpr int GK = kGK;
-    const int dsl = (L.d + KS - 1) / KS;
-    int kspan = (dsl + GK - 1) / GK * GK;
-    const int NCH = kspan >= 2 * GK ? 2 : 1;   // (4 spills beside two accumulator chains)
-    kspan = (kspan + NCH * GK - 1) / (NCH * GK) * (NCH * GK);
-    float* D2 = L.at<float>(ws, L.D2);
-    const size_t plane = size_t(L.n) * L.ldD;
-    int32_t* st = L.at<int32_t>(ws, L.status);
-    int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
-    const dim3 grid(tiles * KS, bt.B);
+    const int T64 = (L.n + 63) / 64;
+    const dim3 grid(T64 * (T64 + 1) / 2, bt.B);
     prof_begin(GLL_K_GRAM, s);
-#define GLL_GRAM(V, N, G)                                                                         \
-    launch_k(gram_lds_kernel<V, N, G>, grid, 512, 0, s, X, L.n, L.d, T, KS, kspan, D2, L.ldD, plane, st, \
-                                                   rc, bt.x, bt.ws)
-    if (vec) {
-        if (NCH == 2) GLL_GRAM(true, 2, GK); else GLL_GRAM(true, 1, GK);
-    } else {
-        if (NCH == 2) GLL_GRAM(false, 2, GK); else GLL_GRAM(false, 1, GK);
-    }
-#undef GLL_GRAM
+    if (vec)
+        launch_k(gram_bf3_kernel<true>, grid, 1024, 0, s, X, L.n, L.d, T64, D2, L.ldD, st, rc, bt.x, bt.ws);
+    else
+        launch_k(gram_bf3_kernel<false>, grid, 1024, 0, s, X, L.n, L.d, T64, D2, L.ldD, st, rc, bt.x, bt.ws);
     prof_end(GLL_K_GRAM, s);
-    return launch_status("knn.hip:launch_gram");
+    return launch_status("knn.hip:launch_gram(bf3)");
 }
 
 hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float* X,
@@ -1548,7 +1097,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     // candidate list capacity: smallest of {16, 32, 64} leaving a re-rank margin >= 4
     const int need = K - 1 + 4;
     const int KC = need <= 16 ? 16 : (need <= 32 ? 32 : 64);
-    if (K - 1 > 64) return hipErrorInvalidValue;
+    if (K - 1 > kMaxKm1) return hipErrorInvalidValue;   // the rescan keeps >= 8 lanes free
     int margin = KC - (K - 1);
     if (margin > 8) margin = 8;
     int kc = K - 1 + margin;

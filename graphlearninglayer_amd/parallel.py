@@ -37,18 +37,27 @@ class PredictionGatherer:
     single gather moves 20 KB, so its ~10-30 us of launch and rendezvous latency, not bytes,
     is the cost; one gather per `every` calls amortises it).
 
-    `add(U)` keeps a reference to this call's U (no copy, no collective); every `every`-th
-    call stacks the pending U's into one (every, m, C) tensor and issues ONE asynchronous
-    all_gather_into_tensor; `flush()` issues it for a partial group.  Completed groups land
-    in `self.gathered` as (world, every, m, C) tensors in call order once `wait()` returns.
-    With one rank (or no process group) it is a no-op that records nothing."""
+    `add(U)` snapshots this call's U (detached, copied on the stream into slot i of the
+    group's (every, m, C) block, so neither the autograd graph nor the saved workspace is
+    kept alive and a later in-place edit of U -- adversarial.py:691 -- does not change what
+    is gathered); the `every`-th call issues ONE asynchronous all_gather_into_tensor of the
+    block; `flush()` issues it for a partial group.  Completed groups land in
+    `self.gathered` as (world, calls, m, C) tensors in call order once `wait()` returns
+    (only the newest `keep` of them when `keep` is set).  With one rank (or no process
+    group) it is a no-op that records nothing."""
 
-    def __init__(self, every: int = 8, group=None):
+    def __init__(self, every: int = 8, group=None, keep=None):
         self.every = max(1, int(every))
         self.group = group
-        self.pending = []
+        self.keep = keep
+        self._block = None      # (every, m, C) snapshots of the current group
+        self._fill = 0
         self.inflight = []      # (out tensor, work)
         self.gathered = []
+
+    @property
+    def pending(self):
+        return [] if self._block is None else list(self._block[: self._fill])
 
     def _active(self) -> bool:
         return (dist.is_available() and dist.is_initialized()
@@ -57,16 +66,28 @@ class PredictionGatherer:
     def add(self, U: torch.Tensor) -> None:
         if not self._active():
             return
-        self.pending.append(U)
-        if len(self.pending) >= self.every:
+        U = U.detach()
+        b = self._block
+        if b is not None and (b.shape[1:] != U.shape or b.dtype != U.dtype
+                              or b.device != U.device):
+            self.flush()
+            b = None
+        if b is None:
+            # a fresh block per group: the previous one may still be read by its collective
+            b = self._block = torch.empty((self.every,) + tuple(U.shape), dtype=U.dtype,
+                                          device=U.device)
+            self._fill = 0
+        b[self._fill].copy_(U)
+        self._fill += 1
+        if self._fill >= self.every:
             self.flush()
 
     def flush(self) -> None:
-        if not self.pending:
+        if self._block is None or self._fill == 0:
             return
         world = dist.get_world_size(self.group)
-        block = torch.stack([u.detach() for u in self.pending]).contiguous()
-        self.pending = []
+        block = self._block[: self._fill]
+        self._block, self._fill = None, 0
         # concatenated along dim 0 (the layout every backend accepts), viewed per rank below
         out = torch.empty((world * block.shape[0],) + tuple(block.shape[1:]), dtype=block.dtype,
                           device=block.device)
@@ -80,3 +101,5 @@ class PredictionGatherer:
             work.wait()
             self.gathered.append(out)
         self.inflight = []
+        if self.keep is not None and len(self.gathered) > self.keep:
+            del self.gathered[: len(self.gathered) - self.keep]

@@ -39,6 +39,9 @@ extern "C" {
 #define GLL_ST_FWD_ITERS 2     /* max forward CG iterations over columns */
 #define GLL_ST_BWD_NONCONV 3   /* adjoint CG columns that hit max_iter */
 #define GLL_ST_BWD_ITERS 4     /* max adjoint CG iterations over columns */
+#define GLL_ST_KNN_RESCAN 5    /* kNN rows whose candidate set failed the Gram error certificate
+                                * and were re-ranked exactly over every column under the bound
+                                * (diagnostic count; the result is exact either way) */
 #define GLL_ST_NWORDS 16
 
 /* gll_problem.flags */
@@ -46,7 +49,7 @@ extern "C" {
 #define GLL_FLAG_GRAM_NARROW 2  /* Gram on 64-tiles even where 128-tiles apply (diagnostic) */
 #define GLL_FLAG_CG_CLASSIC 4   /* per-column CG: two-reduction PCG instead of the single-reduction form (diagnostic) */
 #define GLL_FLAG_CG_PERCOL 8    /* single graphs with m > 1024: per-column CG instead of the whole-GPU CG (diagnostic) */
-#define GLL_FLAG_GRAM_F32 16    /* Gram on the fp32 MFMA kernels instead of the split-bf16 one (diagnostic) */
+#define GLL_FLAG_GRAM_F32 16    /* retired in round 2 with the fp32-MFMA Gram kernels: rejected (GLL_ERR_UNSUPPORTED) */
 #define GLL_FLAG_CG_PIPE 32     /* per-column CG: pipelined PCG (one barrier per iteration) (diagnostic) */
 #define GLL_FLAG_GRAM_NOSPLIT 64 /* small single graphs: unsplit Gram tiles (one D2 plane) (diagnostic) */
 
@@ -55,7 +58,7 @@ typedef struct gll_problem {
     int32_t d;        /* feature dimension */
     int32_t base;     /* labeled rows = label_matrix.shape[0] (GLL.py:32) */
     int32_t C;        /* classes = label_matrix.shape[1] */
-    int32_t K;        /* neighbours incl. self; the reference hard-codes 25 (GLL.py:27) */
+    int32_t K;        /* neighbours incl. self, 1 <= K <= 57; the reference hard-codes 25 (GLL.py:27) */
     int32_t max_iter; /* CG iteration cap per column; 0 => 1000 */
     float tau;        /* diagonal regulariser of Luu (GLL.py:48) */
     float eps;        /* > 0: fixed epsilon (GLL.py:226); <= 0: 'auto' (GLL.py:200-205) */

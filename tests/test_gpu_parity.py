@@ -5,9 +5,11 @@ relative (||a - b||_inf / ||b||_inf) of the reference CPU path on fixed inputs.
   * graph-level parity: the oracle (float64 closed form, pinned to the reference in
     test_oracle_golden.py) is fed the GPU's own kNN lists, so parity of the graph, the
     solves and the gradient is tested independently of fp32 near-ties in the kNN search;
-  * fixture parity: where the GPU kNN sets equal the reference's, U and grad_X are compared
-    with the reference outputs directly;
-  * kNN parity: index sets equal the exact float64 sets except near-ties (rel gap < 1e-5).
+  * fixture parity: the GPU kNN sets must equal the reference's in every row, and U and
+    grad_X are compared with the reference outputs directly for every fixture case;
+  * kNN parity: index sets equal the exact float64 sets (float64 re-rank + the Gram-error
+    certificate); the older near-tie allowance (rel gap < 1e-5) remains only as a looser
+    check beside the exact one where the reference itself is not run.
 """
 import numpy as np
 import pytest
@@ -63,12 +65,15 @@ def test_parity_against_reference_fixture(name):
     eU, eg = O.rel_err(U, Uo), O.rel_err(grad, go)
     assert eU < TOL, f"U vs oracle(gpu knn): {eU:.3e}"
     assert eg < TOL, f"grad vs oracle(gpu knn): {eg:.3e}"
-    # kNN parity against the reference's lists
+    # kNN parity against the reference's own lists: identical sets in every row (the float64
+    # re-rank and the Gram-error certificate make the GPU search exact), so U and grad_X are
+    # compared with the reference outputs directly, in every case -- never skipped
     bad = [i for i, (a, b) in enumerate(zip(ind.tolist(), c.knn.tolist())) if set(a) != set(b)]
-    assert O.knn_set_mismatch(c.X, ind, c.k) == []   # differences only at near-ties
-    if not bad:
-        assert O.rel_err(U, c.U) < TOL
-        assert c.grad_error(grad, O.rel_err) < TOL
+    assert bad == [], f"{len(bad)} rows differ from the reference kNN, first {bad[:8]}"
+    eU_ref, eg_ref = O.rel_err(U, c.U), c.grad_error(grad, O.rel_err)
+    print(f"{name}: U vs reference {eU_ref:.2e}, grad vs reference {eg_ref:.2e}")
+    assert eU_ref < TOL, f"U vs reference: {eU_ref:.3e}"
+    assert eg_ref < TOL, f"grad vs reference: {eg_ref:.3e}"
 
 
 def test_knn_lists_ordered_and_self_first():
@@ -478,3 +483,61 @@ def test_utils_laplace_large_graph_matches_oracle():
     assert O.rel_err(U, Uo) <= TOL
     acc = U_.gl_accuracy(X[:250], train, X[250:], labels[250:])
     assert acc == pytest.approx(100.0 * np.mean(Uo.argmax(1) == labels[250:]), abs=0.05)
+
+
+def _exact_knn_rows(X, ind, k):
+    """Rows whose GPU kNN set differs from the exact float64 set (ties at 1e-12 excused)."""
+    return O.knn_set_mismatch(X, ind, k, rel_gap=1e-12)
+
+
+@pytest.mark.parametrize("offset", [100.0, 1000.0])
+def test_translated_features_exact_knn(offset):
+    """NS features plus a common offset of norm `offset`: |x|^2 >> d^2, the case where an
+    uncentred split-bf16 Gram nominates wrong candidates.  The Gram works on rows centred on
+    row 0 (distance-invariant), the certificate holds, and the kNN sets, U and grad_X match
+    the float64 oracle; no row needs the rescan."""
+    from graphlearninglayer_amd import _lib
+    c = Case("ns_eps1p0_tau0p07_f32")
+    rng = np.random.default_rng(17)
+    v = rng.standard_normal(c.X.shape[1])
+    Xs = (c.X.astype(np.float64) + offset * v / np.linalg.norm(v)).astype(np.float32)
+    g = _gpu_knn(Xs, c.k, c.eps)
+    ind = g["knn_idx"].cpu().numpy()
+    assert _exact_knn_rows(Xs, ind, c.k) == []
+    assert int(g["status"][_lib.ST_KNN_RESCAN].item()) == 0
+    U, grad = _run(Xs, c.Y, c.tau, c.eps, c.k, c.gbar)
+    Uo, st = O.forward(Xs, c.Y, c.tau, c.eps, c.k, knn=(ind.astype(np.int64), None))
+    assert O.rel_err(U, Uo) < TOL
+    assert O.rel_err(grad, O.backward(st, c.gbar)) < TOL
+
+
+def test_far_centre_row_takes_exact_rescan():
+    """Row 0 (the Gram's centre) far from every other row: the split-bf16 error bound then
+    exceeds the neighbour gaps, the certificate fails in (nearly) every row and the exact
+    rescan under the bound runs -- the kNN is still exact and the solve still matches."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
+    X, lab = synth(100, 400, 64, r=1.0, seed=23)
+    X = X.astype(np.float32)
+    X[0] = 300.0 / np.sqrt(64)      # |x_0 - x_i| ~ 300
+    k = 10
+    g = _gpu_knn(X, k, "auto")
+    ind = g["knn_idx"].cpu().numpy()
+    assert int(g["status"][_lib.ST_KNN_RESCAN].item()) > 100
+    assert _exact_knn_rows(X, ind, k) == []
+    Y = one_hot(lab[:100])
+    gb = seeded_gbar(400, 10, 5)
+    U, grad = _run(X, Y, 0.07, "auto", k, gb)
+    Uo, st = O.forward(X, Y, 0.07, "auto", k, knn=(ind.astype(np.int64), None))
+    assert O.rel_err(U, Uo) < TOL
+    assert O.rel_err(grad, O.backward(st, gb)) < TOL
+
+
+@pytest.mark.parametrize("cfg", ["plumbing", "ns", "fullysup"])
+def test_knn_exact_against_float64(cfg):
+    """kNN sets equal the exact float64 sets (no near-tie allowance) at the bench configs."""
+    from graphlearninglayer_amd.synth import CONFIGS, synth
+    c = CONFIGS[cfg]
+    X, _ = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=3)
+    ind = _gpu_knn(X, c["k"], 1.0)["knn_idx"].cpu().numpy()
+    assert _exact_knn_rows(X, ind, c["k"]) == []

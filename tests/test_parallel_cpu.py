@@ -106,3 +106,61 @@ def test_coalesced_gatherer_single_process_is_noop():
     g.add(torch.zeros(3, 2))
     g.wait()
     assert g.gathered == [] and g.pending == []
+
+
+def _snapshot_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = PredictionGatherer(every=2)
+        U = torch.full((4, 3), float(rank), requires_grad=True) * 1.0   # non-leaf, has a graph
+        g.add(U)
+        with torch.no_grad():
+            U.add_(100.0)            # the CW pattern edits the output in place (adversarial.py:691)
+        g.add(U)
+        g.wait()
+        (blk,) = g.gathered
+        assert not blk.requires_grad
+        np.save(os.path.join(out_dir, f"s{rank}.npy"), blk.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gatherer_snapshots_calls_world2(tmp_path):
+    """add() copies U at call time: an in-place edit afterwards changes only later calls."""
+    world = 2
+    mp.spawn(_snapshot_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        got = np.load(tmp_path / f"s{r}.npy")                     # (world, calls, 4, 3)
+        for q in range(world):
+            assert (got[q, 0] == q).all() and (got[q, 1] == q + 100.0).all()
+
+
+def _bench(*args, env=None):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(v, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], env=e,
+                       capture_output=True, text=True, timeout=300)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+def test_bench_launches_its_own_ranks_dry_run():
+    """`bench.py --gpus 2` (the driver's N>1 command without an outer torchrun) starts two
+    ranks itself; rank 0 prints one line with n_gpus 2 and rank-ordered gathers."""
+    rc, out, err = _bench("--gpus", "2", "--dry-run", "--steps", "17", "--warmup", "3")
+    assert rc == 0, err[-2000:]
+    assert out["n_gpus"] == 2 and out["steps"] == 17 and out["dry_run"] is True
+    assert out["gather_check"] == "ok"
+    assert out["config"]["parallelism"] == "dp2"
+
+
+def test_bench_rejects_world_size_mismatch():
+    rc, out, err = _bench("--gpus", "2", "--dry-run", env={"WORLD_SIZE": "1"})
+    assert rc == 2 and out is None and "WORLD_SIZE=1" in err

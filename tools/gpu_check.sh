@@ -15,7 +15,7 @@ run() {  # run <name> <seconds> <cmd...>
 STEPS=${STEPS:-smoke,tests,bench}
 [[ $STEPS == *info* ]] && run info 60 bash -c "rocminfo | grep -E 'Marketing|gfx|Compute Unit' | head -8; nproc; lscpu | grep 'Model name'"
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *tests* ]] && run tests 900 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-}
+[[ $STEPS == *tests* ]] && run tests 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 20 ${BENCH_ARGS:-}
 if [[ $STEPS == *prof* ]]; then
   export TMPDIR=/tmp
