@@ -84,7 +84,10 @@ __global__ __launch_bounds__(256) void edge_coef_kernel(EdgeArgs a) {
     if (lane == 0) a.b[i] = bpart / (2.f * ei * ei);  // modV = d^2 V / (2 eps_i^2), GLL.py:218
 }
 
-// out_i = (sum_e coef_e) x_i - sum_e coef_e x_{col_e};  AUTO selects the coefficient form
+// out_i = sum_e coef_e (x_i - x_{col_e}) in the difference form: translation-invariant like the
+// closed form (the reference's laplacian(S) @ X, GLL.py:146-159, cancels (sum coef) x_i against
+// sum coef x_j in fp32 and loses |x| / |x_i - x_j| of its digits on offset features; the fp32
+// differences of nearby rows are exact).  AUTO selects the coefficient form
 // WIDE (single-graph launches, where occupancy is not the limit): twice the x_j rows in
 // flight per batch -- an NS row's ~13 neighbours in one memory round trip instead of two.
 template <bool AUTO, int ND, bool VEC, bool WIDE>
@@ -114,7 +117,6 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
     f32x4 acc[ND];
 #pragma unroll
     for (int q = 0; q < ND; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float csum = 0.f;
     for (int e0 = beg; e0 < end; e0 += kWave) {
         // lanes own edges: coefficient of edge e0 + lane
         const int e = e0 + lane;
@@ -149,9 +151,8 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
             }
 #pragma unroll
             for (int u = 0; u < EB; ++u) {
-                csum += s[u];
 #pragma unroll
-                for (int q = 0; q < ND; ++q) acc[q] += s[u] * v[u][q];
+                for (int q = 0; q < ND; ++q) acc[q] += s[u] * (xv[q] - v[u][q]);
             }
         }
     }
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
 #pragma unroll
     for (int q = 0; q < ND; ++q) {
         const int k = 4 * lane + 4 * kWave * q;
-        const f32x4 r = csum * xv[q] - acc[q];
+        const f32x4 r = acc[q];
         if constexpr (VEC) {
             if (k < d) __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(oi + k));   // streamed out: not re-read here
         } else {

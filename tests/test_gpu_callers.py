@@ -131,3 +131,40 @@ def test_exploding_gradient_diagnostic(capsys):
     assert "possible exploding gradient" in out and "grad norm:" in out
     torch.cuda.synchronize()
     assert torch.isfinite(g).all()
+
+
+def test_fullysup_step_with_device_base_loader():
+    """§8f-4: the FullySup GL step (FullySup.py:134-157) with the base set drawn from the
+    HBM-resident provider instead of `next(iter(base_loader))`: the draw is a permutation of
+    the base set on the GPU, and the step's prediction and input gradient match the float64
+    oracle chained through the same network."""
+    from graphlearninglayer_amd import GLL
+    from graphlearninglayer_amd.base_data import DeviceBaseLoader
+    g = torch.Generator().manual_seed(0)
+    nb, m, k = 100, 300, 25
+    base_imgs = torch.rand(nb, 3, 8, 8, generator=g)
+    base_lab = torch.arange(nb) % 10
+    imgs = torch.rand(m, 3, 8, 8, generator=g)
+    lab = torch.randint(0, 10, (m,), generator=g)
+    W = torch.randn(192, 32, generator=g, dtype=torch.float64) / 8
+    prov = DeviceBaseLoader(base_imgs, base_lab, device="cuda", seed=5)
+    bi, bl = next(iter(prov))
+    assert bi.is_cuda and sorted(bl.tolist()) == sorted(base_lab.tolist())
+    x = torch.cat((bi, imgs.cuda()), 0).requires_grad_(True)          # FullySup.py:154
+    feats = F.normalize(x.flatten(1).double() @ W.cuda(), dim=1).float()
+    pred = GLL.LaplaceLearningSparseHard.apply(feats, prov.label_matrix(bl), 0.07, 1.0, k)
+    loss = custom_ce_loss(pred, lab.cuda())
+    (gx,) = torch.autograd.grad(loss, [x])
+    # oracle chained through the same network in float64, on the GPU's kNN lists
+    ind = GLL.device_graph(feats.detach(), k, 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    xc = x.detach().cpu().requires_grad_(True)
+    fc = F.normalize(xc.flatten(1).double() @ W, dim=1).float().double()
+    Uo, st = O.forward(fc.detach().numpy(), prov.label_matrix(bl).cpu().numpy(), 0.07, 1.0, k,
+                       knn=(ind, None))
+    assert O.rel_err(pred.detach().cpu().numpy(), Uo) < TOL
+    Ut = torch.from_numpy(Uo).requires_grad_(True)
+    lo = custom_ce_loss(Ut, lab)
+    (gU,) = torch.autograd.grad(lo, [Ut])
+    gf = torch.from_numpy(O.backward(st, gU.numpy()))
+    (gxo,) = torch.autograd.grad(fc, [xc], gf)
+    assert O.rel_err(gx.cpu().numpy(), gxo.numpy()) < TOL
