@@ -64,6 +64,9 @@ def _sink(dev: torch.device):
 
 
 def _warn_from(st):
+    if st[_lib.ST_SOLVE_FAILED]:
+        raise RuntimeError("GLL: a whole-GPU CG solve lost a grid barrier (a workgroup never "
+                           "arrived); its outputs were written as NaN")
     if st[_lib.ST_TINY_EPS]:
         warnings.warn("Epsilon in KNN is very close to zero.", UserWarning)  # GLL.py:240-241
     if st[_lib.ST_FWD_NONCONV]:

@@ -21,8 +21,11 @@ FLAG_CG_PERCOL = 8   # gll_problem.flags: per-column CG for large single graphs 
 FLAG_GRAM_F32 = 16   # gll_problem.flags: retired (fp32-MFMA Gram kernels removed); rejected
 FLAG_CG_PIPE = 32    # gll_problem.flags: pipelined per-column PCG (diagnostic)
 FLAG_GRAM_NOSPLIT = 64   # gll_problem.flags: unsplit Gram tiles for small single graphs (diagnostic)
+FLAG_DIAG_GRID_OVERSUB = 128   # tests: whole-GPU CG grid past co-residency (launch refused)
+FLAG_DIAG_GRID_FAIL = 256      # tests: injected grid-barrier failure (NaN + ST_SOLVE_FAILED)
 ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
 ST_KNN_RESCAN = 5   # kNN rows re-ranked over every column under the Gram error bound
+ST_SOLVE_FAILED = 6   # a whole-GPU CG lost a grid barrier: outputs NaN, raised as an error
 ST_NWORDS = 16
 K_GRAM, K_SELECT, K_FINALIZE, K_CG, K_EDGE, K_GRAD = range(6)
 K_COUNT = 6

@@ -153,7 +153,7 @@ static int forward_impl(const gll_problem* p, int B, const float* X, const void*
     float* U32 = L.at<float>(ws, L.P) + size_t(L.base) * L.C;
     return hip_status(launch_cg_luu(L, bt, ws, L.at<float>(ws, L.rhs), bt.ws, GLL_DT_F32, U, U32,
                                     rtol, max_iter, st + GLL_ST_FWD_NONCONV,
-                                    st + GLL_ST_FWD_ITERS, s));
+                                    st + GLL_ST_FWD_ITERS, st + GLL_ST_SOLVE_FAILED, s));
 }
 
 static int backward_impl(const gll_problem* p, int B, const float* X, void* ws,
@@ -172,7 +172,8 @@ static int backward_impl(const gll_problem* p, int B, const float* X, void* ws,
     float* wU = L.at<float>(ws, L.Wadj) + size_t(L.base) * L.C;
     // adjoint solve: Luu is symmetric, so Luu^-T gbar = Luu^-1 gbar (GLL.py:93)
     hipError_t e = launch_cg_luu(L, bt, ws, gbar, bt.g, g_dtype, nullptr, wU, rtol, max_iter,
-                                 st + GLL_ST_BWD_NONCONV, st + GLL_ST_BWD_ITERS, s);
+                                 st + GLL_ST_BWD_NONCONV, st + GLL_ST_BWD_ITERS,
+                                 st + GLL_ST_SOLVE_FAILED, s);
     if (e != hipSuccess) return GLL_ERR_HIP;
     const bool auto_eps = !(p->eps > 0.f);
     return hip_status(launch_backward_grad(L, bt, ws, X, auto_eps, p->eps, gradX,
@@ -249,10 +250,13 @@ int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const f
     if (m < 1 || C < 1 || !row_ptr || !col || !val || !b || !x) return GLL_ERR_INVALID_ARG;
     if (m > 2048 && C <= 16) {   // whole-GPU cooperative CG (lanes per row from nnz ~ 8 m)
         if (!workspace) return GLL_ERR_INVALID_ARG;
-        return hip_status(launch_cg_grid_csr(m, C, row_ptr, col, val, int64_t(m) * 8, b, x, atol,
-                                             max_iter > 0 ? max_iter : 100000, iters, nonconv,
-                                             static_cast<float*>(workspace),
-                                             static_cast<hipStream_t>(stream)));
+        const hipError_t e = launch_cg_grid_csr(m, C, row_ptr, col, val, int64_t(m) * 8, b, x,
+                                                atol, max_iter > 0 ? max_iter : 100000, iters,
+                                                nonconv, nullptr,
+                                                static_cast<float*>(workspace),
+                                                static_cast<hipStream_t>(stream));
+        if (e != hipErrorNotSupported) return hip_status(e);
+        // past the grid kernel's capacity: per-column CG with the vectors in the workspace
     }
     return hip_status(launch_cg_csr(m, C, row_ptr, col, val, b, x, atol,
                                     max_iter > 0 ? max_iter : 100000, iters, nonconv,

@@ -399,17 +399,22 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
 hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,
                            int y_dtype, float tau, float eps_fixed, hipStream_t s);
 // b: right-hand sides of graph 0, `b_stride` bytes apart (the workspace rhs or gbar)
+// st_failed: the public GLL_ST_SOLVE_FAILED word (whole-GPU CG barrier failure)
 hipError_t launch_cg_luu(const Layout& L, const Batch& bt, void* ws, const void* b,
                          size_t b_stride, int b_dtype, double* out64, float* out32, float rtol,
-                         int max_iter, int32_t* st_nonconv, int32_t* st_iters, hipStream_t s);
+                         int max_iter, int32_t* st_nonconv, int32_t* st_iters,
+                         int32_t* st_failed, hipStream_t s);
+// The whole-GPU CG returns hipErrorNotSupported when no grid configuration holds the system
+// (C > 16 or more rows than the co-resident workgroups can keep in registers): callers then
+// run the per-column kernels with the Krylov vectors in the workspace.
 hipError_t launch_cg_grid_luu(const Layout& L, void* ws, const void* b, int b_dtype,
                               double* out64, float* out32, float rtol, float atol,
                               int max_iter, int32_t* st_nonconv, int32_t* st_iters,
-                              hipStream_t s);
+                              int32_t* st_failed, hipStream_t s);
 hipError_t launch_cg_grid_csr(int m, int C, const int32_t* row_ptr, const int32_t* col,
                               const float* val, int64_t nnz, const float* b, float* x,
                               float atol, int max_iter, int32_t* iters, int32_t* nonconv,
-                              float* ws, hipStream_t s);
+                              int32_t* failed, float* ws, hipStream_t s);
 hipError_t launch_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col,
                          const float* val, const float* b, float* x, float atol, int max_iter,
                          int32_t* iters, int32_t* nonconv, float* gvec, hipStream_t s);

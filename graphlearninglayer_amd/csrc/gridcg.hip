@@ -5,7 +5,9 @@
 // column runs its own PCG with per-column step sizes, and a column is frozen once it meets
 // its tolerance (GLL.py:258-268 masks alpha/beta the same way).
 //
-// One launch of persistent workgroups (G <= #CUs, all resident), grid barriers between phases:
+// One cooperative launch of persistent workgroups (G <= the co-resident capacity the runtime
+// checks: the launch is refused, not queued, when the grid cannot be resident at once), grid
+// barriers between phases:
 //   A  q = A p  (LPR lanes per row, all C columns per gathered entry), partial (p, q)
 //   B  x += a p, r -= a q, z = M r, partial (r, r), (r, z)
 //   C  p = z + b p
@@ -13,6 +15,9 @@
 // workgroup adds all partials in the same fixed order -- so every workgroup derives
 // bitwise identical step sizes and convergence decisions (no broadcast, deterministic).
 // Vectors are m x C row-major fp32 in the workspace (a gathered row is C contiguous floats).
+#include <algorithm>
+#include <cstdio>
+
 #include "gll_internal.h"
 
 namespace gll {
@@ -70,8 +75,10 @@ struct GridCgArgs {
     float* part;             // [G][3][kGCM] partial sums
     unsigned* sync;          // [0] arrivals, [1] failure word (zeroed before the launch)
     int rows_per_wg;
+    int diag_fail;           // GLL_FLAG_DIAG_GRID_FAIL: inject a barrier failure (tests only)
     int32_t* st_iters;
     int32_t* st_nonconv;
+    int32_t* st_failed;      // public GLL_ST_SOLVE_FAILED word
 };
 
 // Hand-off discipline (cdna_hip_programming.md Guideline 16 R1; MI355X_MICROARCH.md
@@ -327,6 +334,7 @@ __global__ __launch_bounds__(kGT) void cg_grid_kernel(Mat A, GridCgArgs a) {
             wg_partials<LPR>(qown ? ppq : f32x4{0.f, 0.f, 0.f, 0.f}, red, mypart + 0 * kGCM, C);
         }
         ok = grid_barrier(a.sync, (++bar) * G, &s_ok);
+        if (a.diag_fail && it == 2) ok = false;   // injected failure (uniform over the grid)
         if (it == 1) GLL_TRACE_PT(3);
         if (!ok) break;
         grid_totals(a.part, G, 0, C, red, s_tot);
@@ -379,6 +387,11 @@ __global__ __launch_bounds__(kGT) void cg_grid_kernel(Mat A, GridCgArgs a) {
         if (it == 1) GLL_TRACE_PT(6);
     }
     GLL_TRACE_PT(1);
+    // a failed grid barrier (a workgroup never arrived within ~1 s) leaves x partial: the
+    // outputs become NaN and GLL_ST_SOLVE_FAILED is raised, so the failure surfaces in the
+    // caller's loss at once and as an exception at the next status check -- never as a
+    // plausible-looking U
+    const float nanf_ = __builtin_nanf("");
 #pragma unroll
     for (int k = 0; k < RPG; ++k) {
         const int u = r0 + grp + k * NG;
@@ -388,8 +401,9 @@ __global__ __launch_bounds__(kGT) void cg_grid_kernel(Mat A, GridCgArgs a) {
             const int c = 4 * li + t;
             if (c < C) {
                 const size_t i = size_t(u) * C + c;
-                if (a.out64) a.out64[i] = double(x[k][t]);
-                if (a.out32) a.out32[i] = x[k][t];
+                const float xv = ok ? x[k][t] : nanf_;
+                if (a.out64) a.out64[i] = double(xv);
+                if (a.out32) a.out32[i] = xv;
             }
         }
     }
@@ -398,6 +412,7 @@ __global__ __launch_bounds__(kGT) void cg_grid_kernel(Mat A, GridCgArgs a) {
         for (int c = 0; c < C; ++c) nonconv += s_active[c] != 0 ? 1 : 0;
         if (a.st_iters) atomicMax(a.st_iters, it);
         if (a.st_nonconv && (nonconv || !ok)) atomicAdd(a.st_nonconv, ok ? nonconv : C);
+        if (!ok && a.st_failed) atomicOr(a.st_failed, 1);
     }
 }
 
@@ -417,6 +432,40 @@ static int cu_count() {
     return cus;
 }
 
+// Workgroups of one kernel instance that can be resident at once on the whole device.
+template <class Mat, int LPR, int RPG>
+static int coresident_capacity() {
+    static int cap = -1;
+    if (cap < 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &nb, reinterpret_cast<const void*>(cg_grid_kernel<Mat, LPR, RPG>), kGT, 0) !=
+            hipSuccess)
+            nb = 1;
+        (void)hipGetLastError();
+        cap = (nb > 0 ? nb : 1) * cu_count();
+    }
+    return cap;
+}
+
+static bool coop_supported() {
+    static int v = -1;
+    if (v < 0) {
+        int dev = 0, a = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&a, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess) a = 0;
+        (void)hipGetLastError();
+        const char* env = getenv("GLL_GRID_COOP");   // diagnostic A/B: 0 = ordinary launch
+        v = (a != 0 && !(env && env[0] == '0')) ? 1 : 0;
+    }
+    return v == 1;
+}
+
+// G workgroups of rows_per_wg rows.  Cooperative launch: the runtime guarantees that all G are
+// resident together or refuses the launch (hipErrorCooperativeLaunchTooLarge), so the grid
+// barrier cannot wait on a workgroup that was never scheduled.  (Without cooperative-launch
+// support: an ordinary launch sized within the occupancy capacity; the bounded barrier then
+// turns a co-residency failure into NaN outputs + GLL_ST_SOLVE_FAILED.)
 template <class Mat, int LPR, int RPG>
 static hipError_t launch_grid(const Mat& A, GridCgArgs a, int G, float* ws, hipStream_t s) {
     a.rows_per_wg = (a.m + G - 1) / G;
@@ -428,23 +477,52 @@ static hipError_t launch_grid(const Mat& A, GridCgArgs a, int G, float* ws, hipS
     a.part = a.Zbuf + size_t(a.m) * a.Cp;
     hipError_t e = hipMemsetAsync(a.sync, 0, 16, s);
     if (e != hipSuccess) return e;
-    launch_k(cg_grid_kernel<Mat, LPR, RPG>, dim3(unsigned(G)), kGT, 0, s, A, a);
+    auto fn = cg_grid_kernel<Mat, LPR, RPG>;
+    if (!coop_supported()) {
+        if (G > coresident_capacity<Mat, LPR, RPG>()) return hipErrorCooperativeLaunchTooLarge;
+        launch_k(fn, dim3(unsigned(G)), kGT, 0, s, A, a);
+        return launch_status("gridcg.hip:launch_grid");
+    }
+    Mat Acopy = A;
+    void* args[] = {&Acopy, &a};
+    const ArmedLaunch armed = g_armed;   // bench timing: events around the launch
+    g_armed = ArmedLaunch{};
+    if (armed.kid >= 0) (void)hipEventRecord(armed.e0, s);
+    e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(unsigned(G)),
+                                   dim3(kGT), args, 0, s);
+    if (armed.kid >= 0) (void)hipEventRecord(armed.e1, s);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        static const bool dbg = getenv("GLL_DEBUG") != nullptr;
+        if (dbg) fprintf(stderr, "gll: gridcg.hip:launch_grid (cooperative, G=%d): %s\n", G,
+                         hipGetErrorString(e));
+        return e;
+    }
     return launch_status("gridcg.hip:launch_grid");
 }
 
 // Lanes per row from the mean row length; rows per lane group (registers) and workgroups:
 // the fewest rows per group that keep the grid within 64 workgroups (barrier cost grows with
-// the arrivals), else within one workgroup per CU.
+// the arrivals), else within the co-resident capacity.  Returns hipErrorNotSupported when no
+// configuration holds the system (rows past capacity x 32 x 8): the caller then runs the
+// per-column kernels with the Krylov vectors in the workspace, which take any size.
+// `oversub` (GLL_FLAG_DIAG_GRID_OVERSUB, tests only) asks for twice the capacity.
 template <class Mat>
 static hipError_t dispatch_grid(const Mat& A, const GridCgArgs& a, int64_t nnz, float* ws,
-                                hipStream_t s) {
+                                bool oversub, hipStream_t s) {
     const int64_t avg = a.m > 0 ? nnz / a.m : 0;
     const int LPR = avg <= 12 ? 4 : 8;
     const int64_t NG = kGT / LPR;
-    const int cus = cu_count();
+    int64_t cap = LPR == 4 ? std::min(coresident_capacity<Mat, 4, 1>(),
+                                            coresident_capacity<Mat, 4, 8>())
+                                 : std::min(coresident_capacity<Mat, 8, 1>(),
+                                            coresident_capacity<Mat, 8, 8>());
+    const char* cap_env = getenv("GLL_GRID_CAP");   // tests: shrink the capacity (read per call)
+    const int64_t cap_lim = cap_env ? std::max(1, atoi(cap_env)) : cap;
+    cap = std::min(cap, cap_lim);
     int rpg = 0;
     int64_t G = 0;
-    for (int lim : {64, cus}) {
+    for (int64_t lim : {std::min<int64_t>(64, cap), cap}) {
         for (int cand : {1, 2, 4, 8}) {
             const int64_t g = (a.m + NG * cand - 1) / (NG * cand);
             if (g <= lim) {
@@ -455,7 +533,11 @@ static hipError_t dispatch_grid(const Mat& A, const GridCgArgs& a, int64_t nnz, 
         }
         if (rpg) break;
     }
-    if (!rpg) return hipErrorInvalidValue;   // > cus * NG * 8 rows: per-column kernels instead
+    if (!rpg) return hipErrorNotSupported;
+    if (oversub) {
+        rpg = 1;
+        G = std::min<int64_t>(2 * cap, a.m);
+    }
     if (G < 1) G = 1;
 #define GLL_GRID(L, R) \
     if (LPR == L && rpg == R) return launch_grid<Mat, L, R>(A, a, int(G), ws, s)
@@ -468,8 +550,8 @@ static hipError_t dispatch_grid(const Mat& A, const GridCgArgs& a, int64_t nnz, 
 hipError_t launch_cg_grid_luu(const Layout& L, void* wsp, const void* b, int b_dtype,
                               double* out64, float* out32, float rtol, float atol,
                               int max_iter, int32_t* st_nonconv, int32_t* st_iters,
-                              hipStream_t s) {
-    if (L.C > kGCM) return hipErrorInvalidValue;
+                              int32_t* st_failed, hipStream_t s) {
+    if (L.C > kGCM) return hipErrorNotSupported;
     LuuRows A{L.at<int32_t>(wsp, L.row_start), L.at<int32_t>(wsp, L.row_len),
               L.at<int32_t>(wsp, L.ucnt),      L.at<int32_t>(wsp, L.col),
               L.at<float>(wsp, L.w),           L.at<float>(wsp, L.diag), L.base};
@@ -485,16 +567,19 @@ hipError_t launch_cg_grid_luu(const Layout& L, void* wsp, const void* b, int b_d
     a.out32 = out32;
     a.st_iters = st_iters;
     a.st_nonconv = st_nonconv;
+    a.st_failed = st_failed;
+    a.diag_fail = (L.flags & GLL_FLAG_DIAG_GRID_FAIL) ? 1 : 0;
     // U-block entries per row ~ 1.5 (K-1) on kNN graphs (mean row length of the union)
     const int64_t nnz_est = int64_t(L.m) * (L.K - 1) * 3 / 2;
-    return dispatch_grid(A, a, nnz_est, L.at<float>(wsp, L.cgv), s);
+    return dispatch_grid(A, a, nnz_est, L.at<float>(wsp, L.cgv),
+                         (L.flags & GLL_FLAG_DIAG_GRID_OVERSUB) != 0, s);
 }
 
 hipError_t launch_cg_grid_csr(int m, int C, const int32_t* row_ptr, const int32_t* col,
                               const float* val, int64_t nnz, const float* b, float* x,
                               float atol, int max_iter, int32_t* iters, int32_t* nonconv,
-                              float* ws, hipStream_t s) {
-    if (C > kGCM) return hipErrorInvalidValue;
+                              int32_t* failed, float* ws, hipStream_t s) {
+    if (C > kGCM) return hipErrorNotSupported;
     CsrRows A{row_ptr, col, val};
     GridCgArgs a{};
     a.m = m;
@@ -507,7 +592,8 @@ hipError_t launch_cg_grid_csr(int m, int C, const int32_t* row_ptr, const int32_
     a.out32 = x;
     a.st_iters = iters;
     a.st_nonconv = nonconv;
-    return dispatch_grid(A, a, nnz, ws, s);
+    a.st_failed = failed;
+    return dispatch_grid(A, a, nnz, ws, false, s);
 }
 
 }  // namespace gll

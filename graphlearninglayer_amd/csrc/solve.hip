@@ -761,7 +761,8 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
 template <typename TB>
 static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const TB* b, size_t bs,
                               double* out64, float* out32, float rtol, int max_iter,
-                              int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
+                              int32_t* st_nonconv, int32_t* st_iters, int32_t* st_failed,
+                              hipStream_t s) {
     const int m = L.m;
     // one persistent launch over the whole GPU (gridcg.hip) for a single graph past the
     // per-column register kernels' sweet spot (m > 2048: 4 ELL slots); measured at stress
@@ -771,8 +772,10 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     if (bt.B == 1 && L.C <= 16 && !(L.flags & GLL_FLAG_CG_PERCOL) &&
         (m > 2048 || (L.flags & GLL_FLAG_CG_GRID))) {
         const int b_dtype = sizeof(TB) == 8 ? GLL_DT_F64 : GLL_DT_F32;
-        return launch_cg_grid_luu(L, ws, b, b_dtype, out64, out32, rtol, 0.f, max_iter,
-                                  st_nonconv, st_iters, s);
+        const hipError_t e = launch_cg_grid_luu(L, ws, b, b_dtype, out64, out32, rtol, 0.f,
+                                                max_iter, st_nonconv, st_iters, st_failed, s);
+        if (e != hipErrorNotSupported) return e;
+        // no grid configuration holds it: per-column kernels below (any m)
     }
 #define GLL_ELL(NT, R, S)                                                                   \
     return (L.flags & GLL_FLAG_CG_CLASSIC)                                                  \
@@ -812,16 +815,17 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
 
 hipError_t launch_cg_luu(const Layout& L, const Batch& bt, void* ws, const void* b,
                          size_t b_stride, int b_dtype, double* out64, float* out32, float rtol,
-                         int max_iter, int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
+                         int max_iter, int32_t* st_nonconv, int32_t* st_iters,
+                         int32_t* st_failed, hipStream_t s) {
     if (L.m <= 0) return hipSuccess;
     hipError_t e;
     prof_begin(GLL_K_CG, s);
     if (b_dtype == GLL_DT_F32)
         e = cg_dispatch(L, bt, ws, static_cast<const float*>(b), b_stride, out64, out32, rtol,
-                        max_iter, st_nonconv, st_iters, s);
+                        max_iter, st_nonconv, st_iters, st_failed, s);
     else if (b_dtype == GLL_DT_F64)
         e = cg_dispatch(L, bt, ws, static_cast<const double*>(b), b_stride, out64, out32, rtol,
-                        max_iter, st_nonconv, st_iters, s);
+                        max_iter, st_nonconv, st_iters, st_failed, s);
     else
         return hipErrorInvalidValue;
     prof_end(GLL_K_CG, s);

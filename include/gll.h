@@ -42,6 +42,9 @@ extern "C" {
 #define GLL_ST_KNN_RESCAN 5    /* kNN rows whose candidate set failed the Gram error certificate
                                 * and were re-ranked exactly over every column under the bound
                                 * (diagnostic count; the result is exact either way) */
+#define GLL_ST_SOLVE_FAILED 6  /* nonzero: a whole-GPU CG lost a grid barrier (a workgroup never
+                                * arrived); that solve's outputs were written as NaN.  The
+                                * Python layer raises RuntimeError on it */
 #define GLL_ST_NWORDS 16
 
 /* gll_problem.flags */
@@ -52,6 +55,10 @@ extern "C" {
 #define GLL_FLAG_GRAM_F32 16    /* retired in round 2 with the fp32-MFMA Gram kernels: rejected (GLL_ERR_UNSUPPORTED) */
 #define GLL_FLAG_CG_PIPE 32     /* per-column CG: pipelined PCG (one barrier per iteration) (diagnostic) */
 #define GLL_FLAG_GRAM_NOSPLIT 64 /* small single graphs: unsplit Gram tiles (one D2 plane) (diagnostic) */
+#define GLL_FLAG_DIAG_GRID_OVERSUB 128 /* tests: size the whole-GPU CG at twice its co-resident
+                                        * capacity -- the cooperative launch must be refused */
+#define GLL_FLAG_DIAG_GRID_FAIL 256    /* tests: inject a grid-barrier failure into the
+                                        * whole-GPU CG (NaN outputs + GLL_ST_SOLVE_FAILED) */
 
 typedef struct gll_problem {
     int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */

@@ -45,6 +45,7 @@ CASES = [
     ("ns", "auto", 0.07, "f32"),
     ("fullysup", 1.0, 0.07, "f32"),
     ("adv", "auto", 0.0, "i64"),
+    ("stress", "auto", 0.07, "f32"),    # BASELINE config 5 (projected grad, ~11 s here)
 ]
 EXTRA = {"adv": dict(base=100, batch=1000, d=200, k=25, r=1.0)}
 FULL_GRAD_MAX_N = 256
@@ -148,14 +149,20 @@ def run_laplace(mod):
 
 
 def main():
+    """python tests/golden/make_golden.py [case-name-prefix ...]  (no argument: every case)"""
+    only = sys.argv[1:]
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     mod = load_reference()
-    lap = run_laplace(mod)
-    path = os.path.join(HERE, "laplace_small.npz")
-    np.savez_compressed(path, **lap)
-    print(f"laplace_small: U max {np.abs(lap['U']).max():.4g} -> {os.path.getsize(path)/1024:.0f} KB")
+    if not only or any("laplace_small".startswith(o) for o in only):
+        lap = run_laplace(mod)
+        path = os.path.join(HERE, "laplace_small.npz")
+        np.savez_compressed(path, **lap)
+        print(f"laplace_small: U max {np.abs(lap['U']).max():.4g} -> "
+              f"{os.path.getsize(path)/1024:.0f} KB")
     for cfg, eps, tau, ydt in CASES:
         name = case_name(cfg, eps, tau, ydt)
+        if only and not any(name.startswith(o) for o in only):
+            continue
         out = run_case(mod, cfg, eps, tau, ydt)
         path = os.path.join(HERE, name + ".npz")
         np.savez_compressed(path, **out)

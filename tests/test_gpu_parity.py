@@ -380,8 +380,9 @@ def test_batched_shared_labels_python_and_cpp_paths_agree():
         assert O.rel_err(outs[0][0][g], Uo) <= TOL
 
 
-def _forward_c_abi(X, Y, k, tau, eps, flags=0):
-    """gll_forward through ctypes with explicit problem flags; returns (U, fwd iterations)."""
+def _forward_c_abi(X, Y, k, tau, eps, flags=0, status=None):
+    """gll_forward through ctypes with explicit problem flags; returns (U, fwd iterations,
+    non-converged columns); `status` (a list) receives the public status words."""
     import ctypes as ct
     from graphlearninglayer_amd import _lib
     GLL = _gll()
@@ -397,6 +398,8 @@ def _forward_c_abi(X, Y, k, tau, eps, flags=0):
     _lib.check(lib.gll_forward(ct.byref(prob), Xd.data_ptr(), Yd.data_ptr(), _lib.GLL_DT_F32,
                                ws.data_ptr(), U.data_ptr(), s), "gll_forward")
     st = ws[: 4 * _lib.ST_NWORDS].view(torch.int32).cpu().tolist()
+    if status is not None:
+        status.extend(st)
     return U.cpu().numpy(), st[_lib.ST_FWD_ITERS], st[_lib.ST_FWD_NONCONV]
 
 
@@ -464,10 +467,10 @@ def test_utils_laplace_matches_reference_fixture():
     Uo = O.laplace(X, train, knn_num=p["knn_num"], epsilon=p["epsilon"], tau=p["tau"],
                    knn=(ind, None))
     assert O.rel_err(U, Uo) <= TOL
-    assert len(O.knn_set_mismatch(X, ind, p["knn_num"])) == 0   # only near-ties may differ
     ref_ind = z["knn"].astype(np.int64)
-    if all(set(a) == set(b) for a, b in zip(ind.tolist(), ref_ind.tolist())):
-        assert O.rel_err(U, z["U"]) <= TOL
+    bad = [i for i, (a, b) in enumerate(zip(ind.tolist(), ref_ind.tolist())) if set(a) != set(b)]
+    assert bad == [], f"{len(bad)} rows differ from the reference kNN, first {bad[:8]}"
+    assert O.rel_err(U, z["U"]) <= TOL          # against the reference pipeline's output
     assert np.mean(U.argmax(1) == z["U"].argmax(1)) >= 0.999
 
 
@@ -541,3 +544,51 @@ def test_knn_exact_against_float64(cfg):
     X, _ = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=3)
     ind = _gpu_knn(X, c["k"], 1.0)["knn_idx"].cpu().numpy()
     assert _exact_knn_rows(X, ind, c["k"]) == []
+
+
+def _grid_case():
+    from graphlearninglayer_amd.synth import one_hot, synth
+    base, m, d, k = 2000, 6000, 64, 10
+    X, lab = synth(base, m, d, r=1.0, seed=5)
+    return X, one_hot(lab[:base]), k
+
+
+def test_grid_cg_oversubscribed_launch_is_refused():
+    """A whole-GPU CG grid larger than the co-resident capacity is refused at launch (the
+    cooperative launch's guarantee) and surfaces as an error -- never as a U computed by a
+    grid whose barrier waited on workgroups that were not resident."""
+    from graphlearninglayer_amd import _lib
+    X, Y, k = _grid_case()
+    with pytest.raises(RuntimeError, match="gll_forward failed"):
+        _forward_c_abi(X, Y, k, 0.07, 1.0, flags=_lib.FLAG_CG_GRID | _lib.FLAG_DIAG_GRID_OVERSUB)
+    torch.cuda.synchronize()   # the device is still healthy: a normal call works
+    U, it, nc = _forward_c_abi(X, Y, k, 0.07, 1.0)
+    assert np.isfinite(U).all() and nc == 0
+
+
+def test_grid_cg_barrier_failure_gives_nan_and_raises():
+    """An (injected) grid-barrier failure writes NaN outputs and raises GLL_ST_SOLVE_FAILED,
+    which the Python layer turns into RuntimeError -- not a partial x as a plausible U."""
+    from graphlearninglayer_amd import _lib
+    GLL = _gll()
+    X, Y, k = _grid_case()
+    st = []
+    U, it, nc = _forward_c_abi(X, Y, k, 0.07, 1.0,
+                               flags=_lib.FLAG_CG_GRID | _lib.FLAG_DIAG_GRID_FAIL, status=st)
+    assert np.isnan(U).all()
+    assert st[_lib.ST_SOLVE_FAILED] != 0 and nc == Y.shape[1]
+    with pytest.raises(RuntimeError, match="grid barrier"):
+        GLL._warn_from(st)
+
+
+def test_grid_cg_past_capacity_falls_back_to_per_column(monkeypatch):
+    """More rows than the co-resident workgroups can hold (capacity shrunk to 4 workgroups
+    through GLL_GRID_CAP): the whole-GPU CG declines and the per-column kernels with the
+    Krylov vectors in the workspace solve the system -- no size limit, same answer."""
+    X, Y, k = _grid_case()
+    monkeypatch.setenv("GLL_GRID_CAP", "4")
+    U, it, nc = _forward_c_abi(X, Y, k, 0.07, 1.0)
+    monkeypatch.delenv("GLL_GRID_CAP")
+    ind = _gpu_knn(X, k, 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, _ = O.forward(X, Y, tau=0.07, epsilon=1.0, K=k, knn=(ind, None))
+    assert nc == 0 and O.rel_err(U, Uo) <= TOL
