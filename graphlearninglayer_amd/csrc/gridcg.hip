@@ -485,6 +485,10 @@ static hipError_t launch_grid(const Mat& A, GridCgArgs a, int G, float* ws, hipS
     }
     Mat Acopy = A;
     void* args[] = {&Acopy, &a};
+    static const bool dbg_launch = getenv("GLL_DEBUG") != nullptr;
+    if (dbg_launch)
+        fprintf(stderr, "gll: grid CG cooperative launch G=%d rows/wg=%d LPR=%d RPG=%d cap=%d\n",
+                G, a.rows_per_wg, LPR, RPG, coresident_capacity<Mat, LPR, RPG>());
     const ArmedLaunch armed = g_armed;   // bench timing: events around the launch
     g_armed = ArmedLaunch{};
     if (armed.kid >= 0) (void)hipEventRecord(armed.e0, s);

@@ -794,15 +794,17 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
 }
 
-// Exact squared distances d(i, c_L)^2 for the candidates c_L held by lanes L in [lo, hi)
-// (ci = -1: no candidate), 8 lanes per candidate across d, PG groups of 8 candidates per
-// sweep with every load in flight.  The differences and the sum are float64 -- the
-// reference's stand-in ranks in float64 -- so the order agrees with it
-// except at relative gaps ~1e-15, and the (i, j) and (j, i) sums run the same lane mapping
-// on negated differences: bitwise symmetric.  Lanes outside [lo, hi) keep `ce`.
-template <bool VEC, int PG>
-__device__ __forceinline__ double exact_d2(const float* __restrict__ X, const float* __restrict__ xi,
-                                           int i, int d, int ci, int lo, int hi, double ce) {
+// Exact squared distances d(i, c_L)^2 = sum_k (x_ik - x_jk)^2 for the candidates c_L held by
+// lanes L in [lo, hi) (ci = -1: no candidate), 8 lanes per candidate across d, PG groups of 8
+// candidates per sweep with every load in flight.  ACC = float: fp32 differences and sums
+// (the fast path); ACC = double: float64 differences and sums -- the reference's stand-in
+// ranks in float64 -- used where fp32 cannot separate two candidates.  Either
+// way the (i, j) and (j, i) sums run the same lane mapping on negated differences: bitwise
+// symmetric for the same ACC.  Lanes outside [lo, hi) keep `ce`.
+template <bool VEC, int PG, typename ACC, int NU = 16>
+__device__ __forceinline__ ACC exact_d2(const float* __restrict__ X, const float* __restrict__ xi,
+                                        int i, int d, int ci, int lo, int hi, ACC ce) {
+    constexpr bool F64 = std::is_same<ACC, double>::value;
     const int lane = lane_id();
     const int grp = lane >> 3, sub = lane & 7;
     for (int p0 = lo; p0 < hi; p0 += 8 * PG) {
@@ -814,41 +816,51 @@ __device__ __forceinline__ double exact_d2(const float* __restrict__ X, const fl
             const bool live = idx < hi && j >= 0;
             xj[g2] = X + size_t(live ? j : i) * d;
         }
-        double part[PG];
+        ACC part[PG];
 #pragma unroll
-        for (int g2 = 0; g2 < PG; ++g2) part[g2] = 0.0;
-        for (int kb = 0; kb < d; kb += 512) {   // 16 steps of 32 features: all loads in flight
-            f32x4 va[16], vb[PG][16];
+        for (int g2 = 0; g2 < PG; ++g2) part[g2] = ACC(0);
+        for (int kb = 0; kb < d; kb += 32 * NU) {   // NU steps of 32 features: loads in flight
+            f32x4 va[NU], vb[PG][NU];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {   // straight-line: every load issued before use
+            for (int u = 0; u < NU; ++u) {   // straight-line: every load issued before use
                 const int k = kb + 32 * u + 4 * sub;
                 va[u] = load4_raw<VEC>(xi, k, d);
 #pragma unroll
                 for (int g2 = 0; g2 < PG; ++g2) vb[g2][u] = load4_raw<VEC>(xj[g2], k, d);
             }
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {   // same order from either end: symmetric in (i, j)
-                const int k = kb + 32 * u + 4 * sub;
-                const f32x4 a = mask4<VEC>(va[u], k, d);
-                const double a0 = a.x, a1 = a.y, a2 = a.z, a3 = a.w;
+            for (int g2 = 0; g2 < PG; ++g2) {
 #pragma unroll
-                for (int g2 = 0; g2 < PG; ++g2) {
-                    const f32x4 b = mask4<VEC>(vb[g2][u], k, d);
-                    const double d0 = a0 - double(b.x), d1 = a1 - double(b.y);
-                    const double d2 = a2 - double(b.z), d3 = a3 - double(b.w);
-                    part[g2] = __builtin_fma(d0, d0, part[g2]);
-                    part[g2] = __builtin_fma(d1, d1, part[g2]);
-                    part[g2] = __builtin_fma(d2, d2, part[g2]);
-                    part[g2] = __builtin_fma(d3, d3, part[g2]);
+                for (int u = 0; u < NU; ++u) {   // same order from either end: symmetric
+                    const int k = kb + 32 * u + 4 * sub;
+                    if constexpr (F64) {
+                        const f32x4 a = mask4<VEC>(va[u], k, d), b = mask4<VEC>(vb[g2][u], k, d);
+                        const double d0 = double(a.x) - double(b.x), d1 = double(a.y) - double(b.y);
+                        const double d2 = double(a.z) - double(b.z), d3 = double(a.w) - double(b.w);
+                        part[g2] = __builtin_fma(d0, d0, part[g2]);
+                        part[g2] = __builtin_fma(d1, d1, part[g2]);
+                        part[g2] = __builtin_fma(d2, d2, part[g2]);
+                        part[g2] = __builtin_fma(d3, d3, part[g2]);
+                    } else {
+                        const f32x4 df = mask4<VEC>(va[u] - vb[g2][u], k, d);
+                        part[g2] += df.x * df.x;
+                        part[g2] += df.y * df.y;
+                        part[g2] += df.z * df.z;
+                        part[g2] += df.w * df.w;
+                    }
                 }
             }
         }
 #pragma unroll
         for (int g2 = 0; g2 < PG; ++g2) {
-            const double tot = group8_sum_d(part[g2]);
+            ACC tot;
+            if constexpr (F64) tot = group8_sum_d(part[g2]);
+            else tot = group8_sum(part[g2]);
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
-                const double v = readlane_d(tot, 8 * g);
+                ACC v;
+                if constexpr (F64) v = readlane_d(tot, 8 * g);
+                else v = readlane_f(tot, 8 * g);
                 if (lane == p0 + 8 * g2 + g) ce = v;
             }
         }
@@ -877,6 +889,76 @@ __device__ __forceinline__ int key_rank(double ce, int ci, int cnt) {
 // rounding of the centring and of the norms -- all below 2^-13 (|a| + |b|)^2 >= 2^-11 |a||b|
 // for d <= 8192 (gll.h caps d at 4096).
 constexpr double kGramErr = 1.0 / 8192.0;
+
+// Float64 re-rank of the candidate list (rare: fp32 cannot separate the boundary pair); a
+// shallow load pipeline (4 steps in flight) keeps its registers under the common path's.
+template <bool VEC>
+__device__ __forceinline__ double refine_d2(const float* __restrict__ X, const float* __restrict__ xi,
+                                            int i, int d, int ci, int kce) {
+    return exact_d2<VEC, 1, double, 4>(X, xi, i, d, ci, 0, kce, __builtin_inf());
+}
+
+struct KnnPick {
+    double d;   // exact d^2 (float64)
+    int j;      // column, -1: none
+};
+
+// Exact rescan of every column with D2_gram <= thr (the certificate failed): candidates in
+// chunks of up to 64 - (K-1) lanes, float64 distances, the K-1 best (by d^2, index) carried
+// in lanes 0..K-2 across chunks (rare path, shallow load pipeline).
+template <bool VEC, int NP>
+__device__ __forceinline__ KnnPick knn_rescan(const float* __restrict__ row, size_t plane, int n,
+                                           int i, const float* __restrict__ X,
+                                           const float* __restrict__ xi, int d, int K,
+                                           double thr, int* s_cand) {
+    const int lane = lane_id();
+    const int F = kWave - (K - 1);          // free lanes per chunk (launch: K-1 <= 56)
+    int bi = -1;                             // running best: lanes 0..K-2
+    double bd = __builtin_inf();
+    for (int jb = 0; jb < n; jb += kWave) {
+        const int j = jb + lane;
+        float v = 0.f;
+        if (j < n) {
+            v = row[j];
+#pragma unroll
+            for (int p = 1; p < NP; ++p) v += row[p * plane + j];
+        }
+        bool take = j < n && j != i && v == v && double(v) <= thr;
+        uint64_t mask = __ballot(take);
+        while (mask) {
+            const int pos = lanes_below(mask);
+            const bool sel = take && pos < F;
+            if (sel) s_cand[pos] = j;
+            const int cnt = __popcll(__ballot(sel));
+            mask &= ~__ballot(sel);
+            take = take && !sel;
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const int off = lane - (K - 1);
+            const int cc = lane < K - 1 ? bi : (off < cnt ? s_cand[off] : -1);
+            double cd = lane < K - 1 ? bd : __builtin_inf();
+            cd = exact_d2<VEC, 1, double, 4>(X, xi, i, d, cc, K - 1, K - 1 + cnt, cd);
+            if (cc < 0) cd = __builtin_inf();
+            const int rk = key_rank(cd, cc, K - 1 + cnt);
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            // keep the K-1 best in rank order: the lane holding rank L goes to LDS slot L
+            const uint64_t live = __ballot(lane < K - 1 + cnt && rk < K - 1 && cc >= 0);
+            if (((live >> lane) & 1ull) != 0) s_cand[rk] = lane;
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const int nl = __popcll(live);
+            const int src = lane < nl ? s_cand[lane] : lane;
+            const int nbi = __shfl(cc, src);
+            const double nbd = shfl_d(cd, src);
+            bi = lane < nl ? nbi : -1;
+            bd = lane < nl ? nbd : __builtin_inf();
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+        }
+    }
+    return KnnPick{bd, bi};
+}
 
 template <int KC, bool VEC, int NP, int PG>
 __global__ __launch_bounds__(256) void knn_select_kernel(
@@ -924,14 +1006,38 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
             kce = kc;
         }
     }
-    // 3) exact float64 squared distances of the candidates.  PG passes per sweep for single
+    // 3) exact squared distances of the candidates, fp32.  PG passes per sweep for single
     //    graphs (one wave per SIMD anyway); batches keep PG = 1 (register pressure).
     const float* xi = X + size_t(i) * d;
-    double ce = exact_d2<VEC, PG>(X, xi, i, d, ci, 0, kce, __builtin_inf());
+    double ce = double(exact_d2<VEC, PG, float>(X, xi, i, d, ci, 0, kce, __builtin_inff()));
     GLL_TRACE_PT(18);
     if (ci < 0) ce = __builtin_inf();
     // 4) rank the candidates by (exact d^2, index); keep the K-1 nearest
     int rank = key_rank(ce, ci, kce);
+    //    fp32 sums of d terms carry <= (d/8 + 3) 2^-24 relative error: where the pair at the
+    //    set boundary (ranks K-2 | K-1) -- or, for auto eps, the pair that decides the kth
+    //    neighbour (K-3 | K-2) -- is closer than 4x that, rank again in float64
+    {
+        const double tol = double(d / 8 + 16) * (1.0 / 4194304.0);
+        auto at_rank = [&](int r) -> double {
+            const uint64_t b = __ballot(lane < kce && ci >= 0 && rank == r);
+            return b ? readlane_d(ce, int(__builtin_ctzll(b))) : __builtin_inf();
+        };
+        bool tie = false;
+        if (K >= 2 && kce > K - 1) {
+            const double a = at_rank(K - 2), b = at_rank(K - 1);
+            tie |= b - a <= tol * b;
+        }
+        if (auto_eps && K >= 3) {
+            const double a = at_rank(K - 3), b = at_rank(K - 2);
+            tie |= b - a <= tol * b;
+        }
+        if (tie) {
+            ce = refine_d2<VEC>(X, xi, i, d, ci, kce);
+            if (ci < 0) ce = __builtin_inf();
+            rank = key_rank(ce, ci, kce);
+        }
+    }
     bool keep = lane < kce && ci >= 0 && rank < K - 1;
     int nkeep = __popcll(__ballot(keep));
 
@@ -940,7 +1046,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     //    |a_j| <= |a_i| + sqrt(dK), D2_gram <= dK + B with B = kGramErr (2|a_i| + sqrt(dK))^2.
     //    tb > dK + B rules that out.  |a_i|^2 = D2[i][0] (row 0 is the Gram's centre, a_0 = 0).
     //    Otherwise (rare: features far from row 0 relative to the neighbour gaps) every
-    //    column with D2_gram <= dK + B is re-ranked exactly, K-1 best kept across chunks.
+    //    column with D2_gram <= dK + B is re-ranked exactly (knn_rescan).
     if (K >= 2 && nkeep == K - 1 && tb < 0x7F800000u) {
         const uint64_t kb = __ballot(keep && rank == K - 2);
         const double dK = readlane_d(ce, int(__builtin_ctzll(kb)));
@@ -952,54 +1058,9 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
         const double thr = dK + kGramErr * r * r;
         if (!(double(__uint_as_float(tb)) > thr)) {
             if (lane == 0) atomicAdd(&status_pub[GLL_ST_KNN_RESCAN], 1);
-            const int F = kWave - (K - 1);          // free lanes per chunk (launch: K-1 <= 56)
-            int bi = -1;                             // running best: lanes 0..K-2
-            double bd = __builtin_inf();
-            for (int jb = 0; jb < n; jb += kWave) {
-                const int j = jb + lane;
-                float v = 0.f;
-                if (j < n) {
-                    v = row[j];
-#pragma unroll
-                    for (int p = 1; p < NP; ++p) v += row[p * plane + j];
-                }
-                bool take = j < n && j != i && v == v && double(v) <= thr;
-                uint64_t mask = __ballot(take);
-                while (mask) {
-                    const int pos = lanes_below(mask);
-                    const bool sel = take && pos < F;
-                    if (sel) s_cand[wv][pos] = j;
-                    const int cnt = __popcll(__ballot(sel));
-                    mask &= ~__ballot(sel);
-                    take = take && !sel;
-                    __builtin_amdgcn_wave_barrier();
-                    asm volatile("" ::: "memory");
-                    const int off = lane - (K - 1);
-                    int cc = lane < K - 1 ? bi : (off < cnt ? s_cand[wv][off] : -1);
-                    double cd = lane < K - 1 ? bd : __builtin_inf();
-                    cd = exact_d2<VEC, 1>(X, xi, i, d, cc, K - 1, K - 1 + cnt, cd);
-                    if (cc < 0) cd = __builtin_inf();
-                    const int rk = key_rank(cd, cc, K - 1 + cnt);
-                    __builtin_amdgcn_wave_barrier();
-                    asm volatile("" ::: "memory");
-                    // keep the K-1 best in rank order: indices through LDS, distances by
-                    // readlane of the lane that holds rank L
-                    const uint64_t live = __ballot(lane < K - 1 + cnt && rk < K - 1 && cc >= 0);
-                    if (((live >> lane) & 1ull) != 0) s_cand[wv][rk] = lane;
-                    __builtin_amdgcn_wave_barrier();
-                    asm volatile("" ::: "memory");
-                    const int nl = __popcll(live);
-                    const int src = lane < nl ? s_cand[wv][lane] : lane;
-                    const int nbi = __shfl(cc, src);
-                    const double nbd = shfl_d(cd, src);
-                    bi = lane < nl ? nbi : -1;
-                    bd = lane < nl ? nbd : __builtin_inf();
-                    __builtin_amdgcn_wave_barrier();
-                    asm volatile("" ::: "memory");
-                }
-            }
-            ci = bi;
-            ce = bd;
+            const KnnPick pk = knn_rescan<VEC, NP>(row, plane, n, i, X, xi, d, K, thr, s_cand[wv]);
+            ci = pk.j;
+            ce = pk.d;
             kce = K - 1;
             rank = key_rank(ce, ci, kce);
             keep = lane < kce && ci >= 0 && rank < K - 1;

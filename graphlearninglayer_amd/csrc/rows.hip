@@ -5,8 +5,9 @@
 // split (GLL.py:29,37-38,48).  One wave per graph row i (K3 row_build_kernel):
 //   * forward entries: i's own kNN list (valid = d > 0; sparse.find drops zeros, GLL.py:198);
 //   * reverse entries: every l that listed i (pushed by knn_select_kernel onto i's reverse
-//     list, spilling to the overflow list past RCAP), minus those already in i's own list:
-//     the union pattern of GLL.py:197 (distances are bitwise symmetric, so max = either);
+//     list, spilling to the overflow list past RCAP); a reverse entry already in i's own list
+//     (a mutual pair) keeps max(d_ij, d_ji): the union-max of GLL.py:197.  (The two
+//     distances agree bitwise unless one row refined its ranking in float64, knn.hip);
 //   * the row is staged in LDS (global scratch for hub rows), rank-sorted by column --
 //     deterministic whatever order the atomics produced -- and written to its slot
 //     (row_start, row_len; hub rows take a bump-allocated range);
@@ -121,14 +122,19 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
         const bool live = r < nr;
         const int ri = !live ? -1 : (r0 == 0 ? pri : a.rev_idx[size_t(i) * a.RCAP + r]);
         const float rd = !live ? 0.f : (r0 == 0 ? prd : a.rev_d2[size_t(i) * a.RCAP + r]);
-        bool dup = false;
-        for (int t = 0; t < Km1; ++t) dup |= (ri == readlane_i(fself, t));
-        const bool keep = live && !dup;
+        int tpos = -1;
+        for (int t = 0; t < Km1; ++t) tpos = (ri == readlane_i(fself, t)) ? t : tpos;
+        const bool keep = live && tpos < 0;
         const uint64_t mk = __ballot(keep);
         if (keep) {
             const int p = L + lanes_below(mk);
             scol[p] = ri;
             sd2[p] = rd;
+        }
+        if (live && tpos >= 0) {   // mutual pair: union-max (non-negative float bits order)
+            if constexpr (!LDS) __threadfence();
+            const int pt = __popcll(fmask & ((1ull << tpos) - 1ull));
+            atomicMax(reinterpret_cast<unsigned*>(sd2) + pt, __float_as_uint(rd));
         }
         L += __popcll(mk);
     }
@@ -141,14 +147,19 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
             const int oj = live ? a.ovf[3 * q] : -1;
             const int oi = live ? a.ovf[3 * q + 1] : -1;
             const float od = live ? __int_as_float(a.ovf[3 * q + 2]) : 0.f;
-            bool dup = false;
-            for (int t = 0; t < Km1; ++t) dup |= (oi == readlane_i(fself, t));
-            const bool keep = live && oj == i && !dup;
+            int tpos = -1;
+            for (int t = 0; t < Km1; ++t) tpos = (oi == readlane_i(fself, t)) ? t : tpos;
+            const bool keep = live && oj == i && tpos < 0;
             const uint64_t mk = __ballot(keep);
             if (keep) {
                 const int p = L + lanes_below(mk);
                 scol[p] = oi;
                 sd2[p] = od;
+            }
+            if (live && oj == i && tpos >= 0) {   // mutual pair: union-max
+                if constexpr (!LDS) __threadfence();
+                const int pt = __popcll(fmask & ((1ull << tpos) - 1ull));
+                atomicMax(reinterpret_cast<unsigned*>(sd2) + pt, __float_as_uint(od));
             }
             L += __popcll(mk);
         }
