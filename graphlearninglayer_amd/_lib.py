@@ -23,6 +23,8 @@ FLAG_CG_PIPE = 32    # gll_problem.flags: pipelined per-column PCG (diagnostic)
 FLAG_GRAM_NOSPLIT = 64   # gll_problem.flags: unsplit Gram tiles for small single graphs (diagnostic)
 FLAG_DIAG_GRID_OVERSUB = 128   # tests: whole-GPU CG grid past co-residency (launch refused)
 FLAG_DIAG_GRID_FAIL = 256      # tests: injected grid-barrier failure (NaN + ST_SOLVE_FAILED)
+FLAG_CG_ELL = 512   # gll_problem.flags: register-ELL per-column CG where the balanced one runs
+FLAG_CG_VR = 1024   # gll_problem.flags: balanced (virtual-row) per-column CG wherever it fits
 ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
 ST_KNN_RESCAN = 5   # kNN rows re-ranked over every column under the Gram error bound
 ST_SOLVE_FAILED = 6   # a whole-GPU CG lost a grid barrier: outputs NaN, raised as an error

@@ -1,6 +1,6 @@
 // api.hip -- the extern "C" boundary declared in include/gll.h.
 //
-// Orchestrates the kernels of knn.hip, graph.hip, cg.hip and grad.hip on the caller's
+// Orchestrates the kernels of knn.hip, rows.hip, solve.hip / gridcg.hip and grad.hip on the caller's
 // stream.  No allocation, no host synchronisation: the caller owns the workspace (the
 // Python mirror takes it from torch's caching allocator) and keeps it alive from
 // gll_forward to gll_backward, as the reference keeps its graph on ctx (GLL.py:69-70).

@@ -34,6 +34,33 @@ inline int ell_slots(int m) {
     return m <= 512 ? 24 : (m <= 2048 ? 16 : (m <= 4096 ? 4 : 0));
 }
 
+// Balanced per-column CG (solve.hip cg_vr_kernel): the U block of each row cut into "virtual
+// rows" of kVS entries.  row_build writes them pre-packed for it, kVrSlot bytes per virtual
+// row (kVS 16-bit LDS byte offsets of the columns, then kVS fp32 weights, zero-padded), at
+// most kVrMax(K) of them per U row (row u's j-th at slot u * kVrMax + j); longer rows keep
+// their tail in the CSR only.  vr_threads(L) > 0 <=> the per-column solves of this problem
+// run that kernel (with vr_threads(L) virtual rows per thread): a host-side function of the
+// problem alone, so row_build and the CG agree without a device round trip.
+constexpr int kVS = 8;
+constexpr int kVrSlot = kVS * 2 + kVS * 4;   // 48 B
+// threads of the balanced kernel: 512, up to 10 virtual rows each in 256 VGPRs (1024 threads
+// hold at most 5 in 128 VGPRs and spilled: 118 against 66 us per FullySup solve)
+constexpr int kVrNT = 512;
+inline int vr_max_per_row(int K) { return ((K - 1) + 4 * (K - 1) + 8 + kVS - 1) / kVS; }
+inline int vr_threads(int n, int m, int K, int flags) {
+    if (m <= 0 || m > 4 * kVrNT || (flags & GLL_FLAG_CG_ELL)) return 0;
+    if (flags & (GLL_FLAG_CG_CLASSIC | GLL_FLAG_CG_PIPE)) return 0;
+    // kNN union rows hold ~1.4 (K-1) entries, a fraction m/n of them in the U block
+    const double len = 1.4 * (K - 1) * double(m) / double(n);
+    if (len <= 12.0 && !(flags & GLL_FLAG_CG_VR)) return 0;
+    const double v = m * (len / kVS + 0.5);
+    int rv = int((v + kVrNT - 1) / kVrNT);
+    // tests: force the register capacity (4 at K = 25 puts most rows on the CSR spill path)
+    const char* force = getenv("GLL_VR_RV");
+    if (force) rv = atoi(force);
+    return rv <= 4 ? 4 : (rv <= 8 ? 8 : (rv <= 10 ? 10 : 0));
+}
+
 // ---------------------------------------------------------------------------------------
 // In-kernel timestamps (diagnostic builds only: build.py --trace defines GLL_TRACE and
 // writes libgll_trace.so; the product library compiles these to nothing).  Per translation
@@ -124,6 +151,9 @@ struct Layout {
     size_t tmp_col, tmp_d2, col, w, d2e, deg, ucnt, diag, rhs, P, Wadj, S, b, cgv, total;
     int SE;           // ELL slots per U row (ell_slots)
     size_t ell_col, ell_w;
+    int RV;           // balanced CG: virtual rows per thread (vr_threads), 0 = not used
+    int VRM;          // balanced CG: virtual-row slots per U row (vr_max_per_row)
+    size_t vr;        // [m][VRM] packed virtual rows (kVrSlot bytes each)
 
     explicit Layout(const gll_problem& p) {
         n = p.n; d = p.d; base = p.base; C = p.C;
@@ -164,6 +194,9 @@ struct Layout {
         SE = ell_slots(m);
         ell_col = take(size_t(SE) * m * 4);   // [SE][m] U-block columns (U index), 0-padded
         ell_w = take(size_t(SE) * m * 4);     // [SE][m] weights W_uj, 0-padded
+        RV = vr_threads(n, m, K, flags);
+        VRM = RV ? vr_max_per_row(K) : 0;
+        vr = take(size_t(m) * VRM * kVrSlot);
         P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)
         Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
         S = take(size_t(Etot) * 4);        // per-edge coefficient (auto eps only)

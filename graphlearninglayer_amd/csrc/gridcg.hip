@@ -539,8 +539,10 @@ static hipError_t dispatch_grid(const Mat& A, const GridCgArgs& a, int64_t nnz, 
     }
     if (!rpg) return hipErrorNotSupported;
     if (oversub) {
+        // one row per workgroup: far past what the hardware can hold at once (at most 8
+        // workgroups of kGT threads per CU), whatever the occupancy query under-reports
         rpg = 1;
-        G = std::min<int64_t>(2 * cap, a.m);
+        G = std::min<int64_t>(a.m, int64_t(1) << 20);
     }
     if (G < 1) G = 1;
 #define GLL_GRID(L, R) \

@@ -53,6 +53,8 @@ struct RowArgs {
     int32_t* ell_col;   // [SE][m] column-major U slices for the CG (SE = 0: none)
     float* ell_w;
     int SE, m;
+    char* vr;           // [m][VRM] packed virtual rows of the balanced CG (VRM = 0: none)
+    int VRM;
     size_t wss;   // batched launches: workspace stride between graphs (bytes)
 
     __device__ void to_graph() {   // move every workspace pointer to graph blockIdx.y
@@ -79,6 +81,7 @@ struct RowArgs {
         Wadj = gshift(Wadj, wss);
         ell_col = gshift(ell_col, wss);
         ell_w = gshift(ell_w, wss);
+        vr = gshift(vr, wss);
     }
 };
 
@@ -217,6 +220,23 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
             const float we = live ? ow[e] : 0.f;
             a.ell_col[size_t(lane) * a.m + u] = c;
             a.ell_w[size_t(lane) * a.m + u] = we;
+        }
+    }
+    if (i >= a.base && a.VRM > 0) {
+        // the U block as packed virtual rows of kVS entries for the balanced CG (solve.hip
+        // cg_vr_kernel): 16-bit LDS byte offsets of the columns, then the weights, the last
+        // one zero-padded; rows past VRM of them keep their tail in the CSR only
+        const int u = i - a.base, nu = L - nlab;
+        const int nv = min((nu + kVS - 1) / kVS, a.VRM);
+        char* slots = a.vr + size_t(u) * a.VRM * kVrSlot;
+        for (int q = lane; q < nv * kVS; q += kWave) {
+            const bool live = q < nu;
+            const int e = nlab + (live ? q : 0);
+            const int cu = ocol[e] - a.base;
+            const float we = ow[e];
+            char* sl = slots + size_t(q / kVS) * kVrSlot;
+            reinterpret_cast<uint16_t*>(sl)[q % kVS] = live ? uint16_t(cu * 4) : uint16_t(0);
+            reinterpret_cast<float*>(sl + kVS * 2)[q % kVS] = live ? we : 0.f;
         }
     }
     if (ypre) {
@@ -369,6 +389,8 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     a.ell_w = L.at<float>(ws, L.ell_w);
     a.SE = L.SE;
     a.m = L.m;
+    a.vr = L.at<char>(ws, L.vr);
+    a.VRM = L.VRM;
     a.wss = bt.ws;
     dim3 grid((L.n + 3) / 4, bt.B);
     prof_begin(GLL_K_FINALIZE, s);

@@ -1,4 +1,4 @@
-// cg.hip -- Jacobi-preconditioned conjugate gradients on Luu (and on a general CSR).
+// solve.hip -- Jacobi-preconditioned conjugate gradients on Luu (and on a general CSR).
 //
 // Replaces the SuperLU `spsolve(Luu, -Lul Y)` of the forward (/root/reference/GLL.py:53)
 // and `spsolve(Luu, grad_output)` of the backward (GLL.py:93); the algorithm is the
@@ -13,13 +13,15 @@
 // over the sorted CSR of the symmetric kNN graph (labeled columns first, so the U block of
 // a row is a suffix of the row).
 //
-// cg_ell_kernel (m <= 4096): the iteration is latency-bound, so a thread owns R rows and
-// keeps everything about them in registers: x, r, p, Ap, M^-1, diag AND the first S
-// entries of each row's U block as an ELL slice (column, weight), zero-padded so the SpMV
-// gathers are branch-free and all S are in flight at once (entries beyond S are read from
-// the CSR).  Only p is published through LDS for the gathers.  Dot products are DPP wave
-// reductions plus one LDS exchange across waves; an iteration has three barriers.
-// cg_lds_kernel: vectors in LDS or global memory, for systems larger than that.
+// Per-column kernels (cg_dispatch picks one; single graphs with m > 2048 take the whole-GPU
+// CG of gridcg.hip):
+//   cg_ell_kernel (short U rows, m <= 4096): a thread owns R rows and keeps everything about
+//     them in registers, including the first S entries of each U row as an ELL slice; entries
+//     past S are compacted into LDS.  Single-reduction (Chronopoulos-Gear) PCG: one fused
+//     three-value exchange and one publish barrier per iteration.
+//   cg_vr_kernel (long U rows: K = 25, the FullySup shape): the U block cut into "virtual
+//     rows" of 8 entries dealt out evenly to the threads (see its comment).
+//   cg_lds_kernel: vectors in LDS or global memory, for systems larger than either.
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -636,6 +638,310 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     GLL_TRACE_PT(9);
 }
 
+// --------------------------------------------------------------------------------------
+// Balanced per-column CG for long U rows (cg_vr_kernel).
+//
+// At K = 25 (the FullySup caller, FullySup.py:156) a U row of Luu holds 27 entries on average
+// and up to ~75, so a thread-per-row SpMV loops every wave to its longest row, and past the
+// register slots each entry costs three LDS operations (column, weight, gathered value).
+// Here the U block is cut into "virtual rows" of kVS = 8 consecutive entries (a row of L
+// entries gives ceil(L/8)), which row_build writes pre-packed (16-bit LDS byte offsets of the
+// columns, then the weights; gll_internal.h kVrSlot).  The virtual rows -- not the rows -- are
+// dealt out to the threads, v = j * NT + tid for j < RV, and held in registers for the whole
+// solve.  An SpMV is then one LDS gather per entry, the same count for every thread, plus one
+// partial sum per virtual row written to LDS.
+//
+// The row sums of A u are needed only after the iteration's reduction barrier (for the
+// recurrence s = w + beta s), so they are read there from the partials -- no extra barrier.
+// The (w, u) product the reduction needs before that barrier is formed per virtual row
+// instead: (w, u) = sum_rows diag u^2 - sum_v u_row(v) part_v.
+// Fixed partition and fixed summation order: deterministic.  Virtual rows past the register
+// capacity NT x RV (an underestimated size) or past the VRM slots of a row (hubs) are summed
+// by their row's thread from the CSR.
+// --------------------------------------------------------------------------------------
+template <int NT, int R, int RV, typename TB>
+__global__ __launch_bounds__(NT) void cg_vr_kernel(
+    int m, int C, int base, int VRM, const int32_t* __restrict__ row_start,
+    const int32_t* __restrict__ row_len, const int32_t* __restrict__ ucnt,
+    const int32_t* __restrict__ col, const float* __restrict__ wv, const float* __restrict__ diag,
+    const char* __restrict__ vrs, const TB* __restrict__ bsrc, double* __restrict__ out64,
+    float* __restrict__ out32, float rtol, int max_iter, int32_t* __restrict__ st_nonconv,
+    int32_t* __restrict__ st_iters, size_t wss, size_t bs, size_t us, size_t sts) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    row_start = gshift(row_start, wss);
+    row_len = gshift(row_len, wss);
+    ucnt = gshift(ucnt, wss);
+    col = gshift(col, wss);
+    wv = gshift(wv, wss);
+    diag = gshift(diag, wss);
+    vrs = gshift(vrs, wss);
+    bsrc = gshift(bsrc, bs);
+    out64 = gshift_br(out64, us);
+    out32 = gshift_br(out32, wss);
+    st_nonconv = gshift_br(st_nonconv, sts);
+    st_iters = gshift_br(st_iters, sts);
+    constexpr int VCAP = NT * RV;
+    const int c = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int mp4 = (m + 3) & ~3;
+    float* red = smem;                                   // 96 floats of reduction scratch
+    int* scan = reinterpret_cast<int*>(smem + 96);       // 16 ints of scan scratch
+    float* P_ = smem + 128;                              // the published vector u
+    // partial sums, row-padded: row u's at vpart[vpad_u ..), vpad_u 16-B aligned, so the row
+    // sums read them four at a time
+    float* vpart = P_ + mp4;                             // VCAP + 4 mp4
+    int* vmap = reinterpret_cast<int*>(vpart + VCAP + 4 * mp4);   // VCAP: (row << 10) | (j << 4) | len
+    int* vpad = vmap + VCAP;                             // mp4: row u's first partial
+    GLL_TRACE_SCOPE(0);
+    GLL_TRACE_PT(0);
+
+    // ---- rows this thread owns (u = tid + NT q): setup loads all issued together
+    int ulen[R], est[R], vs[R], nvc[R], sps[R], spe[R], vp[R];
+    float dg[R], bv[R], mi[R], x[R], r[R], p[R], sv[R], uu[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int u = tid + NT * q;
+        const int uc = u < m ? u : 0;
+        ulen[q] = ucnt[uc];
+        est[q] = row_start[base + uc] + row_len[base + uc];
+        dg[q] = diag[uc];
+        bv[q] = to_f32(bsrc[size_t(uc) * C + c]);
+    }
+    int tv = 0, tp = 0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        if (tid + NT * q >= m) {
+            ulen[q] = 0;
+            dg[q] = 0.f;
+        }
+        est[q] -= ulen[q];   // the U block is the row's sorted suffix
+        const int nv = min((ulen[q] + kVS - 1) / kVS, VRM);
+        tv += nv;
+        tp += (nv + 3) & ~3;
+    }
+    int V = 0, VP = 0;
+    int v0 = block_excl_scan<NT>(tv, scan, V);
+    __syncthreads();   // the scan scratch is reused
+    int p0 = block_excl_scan<NT>(tp, scan, VP);
+    float rz = 0.f, bb = 0.f;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int u = tid + NT * q;
+        const int nv = min((ulen[q] + kVS - 1) / kVS, VRM);
+        vs[q] = v0;
+        vp[q] = p0;
+        if (u < m) vpad[u] = p0;
+        p0 += (nv + 3) & ~3;
+        for (int j = 0; j < nv && v0 + j < VCAP; ++j)
+            vmap[v0 + j] = (u << 10) | (j << 4) | min(kVS, ulen[q] - kVS * j);
+        nvc[q] = v0 + nv <= VCAP ? nv : (v0 < VCAP ? VCAP - v0 : 0);
+        if (nvc[q] == 0) vp[q] = 0;   // no partials held (past the capacity): stay in bounds
+        sps[q] = est[q] + kVS * nvc[q];   // entries past the held virtual rows: from the CSR
+        spe[q] = est[q] + ulen[q];
+        v0 += nv;
+        mi[q] = dg[q] > 0.f ? 1.f / dg[q] : 0.f;
+        r[q] = mi[q] > 0.f ? bv[q] : 0.f;   // zero-diagonal rows are decoupled: x = 0
+        x[q] = sv[q] = 0.f;
+        p[q] = uu[q] = mi[q] * r[q];
+        if (u < m) P_[u] = uu[q];
+        rz += r[q] * uu[q];
+        bb += r[q] * r[q];
+    }
+    // wave-uniform bound of the partial sums each row reads after the reduction
+    int nvmax[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) nvmax[q] = wave_max_int(nvc[q]);
+    GLL_TRACE_PT(1);
+    __syncthreads();
+    // ---- this thread's virtual rows, packed by row_build: 3 x 16-B loads each, consecutive
+    // threads on consecutive virtual rows
+    uint32_t cpk[RV][kVS / 2];
+    float ew[RV][kVS];
+    int vrow[RV], vmax[RV], pidx[RV];
+    const int Vlive = V < VCAP ? V : VCAP;
+#pragma unroll
+    for (int j = 0; j < RV; ++j) {
+        const int v = j * NT + tid;
+        const int info = vmap[v < Vlive ? v : 0];
+        const int len = v < Vlive ? (info & 15) : 0;
+        vrow[j] = v < Vlive ? (info >> 10) : 0;
+        pidx[j] = v < Vlive ? vpad[info >> 10] + ((info >> 4) & 63) : VCAP + 4 * mp4 - 1;
+        const int slot = v < Vlive ? (info >> 10) * VRM + ((info >> 4) & 63) : 0;
+        const uint4 cw = *reinterpret_cast<const uint4*>(vrs + size_t(slot) * kVrSlot);
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(vrs + size_t(slot) * kVrSlot + 16);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(vrs + size_t(slot) * kVrSlot + 32);
+        // a dead slot loads virtual row 0: masked through an opaque mask (a select on the
+        // loaded values would let the compiler sink the loads into a branch)
+        uint32_t mk = v < Vlive ? 0xffffffffu : 0u;
+        asm volatile("" : "+v"(mk));
+        cpk[j][0] = cw.x & mk;
+        cpk[j][1] = cw.y & mk;
+        cpk[j][2] = cw.z & mk;
+        cpk[j][3] = cw.w & mk;
+        ew[j][0] = __uint_as_float(__float_as_uint(w0.x) & mk);
+        ew[j][1] = __uint_as_float(__float_as_uint(w0.y) & mk);
+        ew[j][2] = __uint_as_float(__float_as_uint(w0.z) & mk);
+        ew[j][3] = __uint_as_float(__float_as_uint(w0.w) & mk);
+        ew[j][4] = __uint_as_float(__float_as_uint(w1.x) & mk);
+        ew[j][5] = __uint_as_float(__float_as_uint(w1.y) & mk);
+        ew[j][6] = __uint_as_float(__float_as_uint(w1.z) & mk);
+        ew[j][7] = __uint_as_float(__float_as_uint(w1.w) & mk);
+        vmax[j] = wave_max_int(len);
+    }
+    GLL_TRACE_PT(3);
+    const char* Pb = reinterpret_cast<const char*>(P_);
+    // A u over this thread's virtual rows: partials to LDS, returns sum_v u_row(v) part_v
+    auto spmv = [&]() {
+        float dl = 0.f;
+        // the packed offsets are "redefined" here so the compiler cannot hoist their unpacked
+        // halves out of the iteration loop (that doubles the registers they take)
+#pragma unroll
+        for (int j = 0; j < RV; ++j)
+#pragma unroll
+            for (int h = 0; h < kVS / 2; ++h) asm volatile("" : "+v"(cpk[j][h]));
+#pragma unroll
+        for (int j = 0; j < RV; ++j) {
+            if (vmax[j] > 0) {
+                float pv[kVS];
+#pragma unroll
+                for (int k0 = 0; k0 < kVS; k0 += 4) {
+                    if (k0 < vmax[j]) {
+#pragma unroll
+                        for (int k = k0; k < k0 + 4; ++k) {
+                            const uint32_t off = (k & 1) ? (cpk[j][k >> 1] >> 16)
+                                                         : (cpk[j][k >> 1] & 0xffffu);
+                            pv[k] = *reinterpret_cast<const float*>(Pb + off);
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = k0; k < k0 + 4; ++k) pv[k] = 0.f;
+                    }
+                }
+                const float ur = P_[vrow[j]];
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < kVS; ++k) acc += ew[j][k] * pv[k];
+                vpart[pidx[j]] = acc;
+                dl += ur * acc;
+            }
+            // one virtual row's gathers in flight at a time: hoisting all RV x 8 spills
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return dl;
+    };
+    // entries past the held virtual rows (rare): this row's thread sums them from the CSR
+    auto spill = [&](int q) {
+        float acc = 0.f;
+        for (int e = sps[q]; e < spe[q]; ++e) acc += wv[e] * P_[col[e] - base];
+        return acc;
+    };
+    // after the reduction barrier: (A u)_row = diag u - sum of the row's partials; the loads
+    // of every row of the thread are issued together, four partials per row per step
+    // the first 8 of a row's partials (rows up to 64 entries) come in two 16-B loads per row,
+    // every row's issued before any is used; longer rows loop over the rest
+    const int vplim = VCAP + 4 * mp4 - 4;
+    auto rowsums = [&](float* wr, const float* spl) {
+        f32x4 pv[R][2];
+#pragma unroll
+        for (int q = 0; q < R; ++q)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                pv[q][h] = *reinterpret_cast<const f32x4*>(vpart + min(vp[q] + 4 * h, vplim));
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            float acc = 0.f;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                acc += 4 * h + 0 < nvc[q] ? pv[q][h].x : 0.f;
+                acc += 4 * h + 1 < nvc[q] ? pv[q][h].y : 0.f;
+                acc += 4 * h + 2 < nvc[q] ? pv[q][h].z : 0.f;
+                acc += 4 * h + 3 < nvc[q] ? pv[q][h].w : 0.f;
+            }
+            for (int t = 8; t < nvmax[q]; ++t) acc += t < nvc[q] ? vpart[vp[q] + t] : 0.f;
+            wr[q] = dg[q] * uu[q] - (acc + spl[q]);
+        }
+    };
+
+    int phase = 0;
+    int it = 0;
+    bool conv;
+    // pre-step: w0 = A u0, gamma0 = (r,u), delta0 = (w,u)
+    float spl[R];
+    float dl = -spmv();
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        spl[q] = spill(q);
+        dl += dg[q] * uu[q] * uu[q] - uu[q] * spl[q];
+    }
+    block_sum3<NT>(rz, bb, dl, red, phase);
+    rowsums(sv, spl);
+    GLL_TRACE_PT(4);
+    const float tol2 = rtol * rtol * bb;
+    conv = !(bb > 0.f);
+    float gam = rz;
+    float alpha = dl > 0.f ? gam / dl : 0.f;
+    if (!(dl > 0.f)) alpha = -1.f;   // breakdown before the first step
+    while (!conv && alpha > 0.f && it < max_iter) {
+        ++it;
+        GLL_TRACE_CYC(10);
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            x[q] += alpha * p[q];
+            r[q] -= alpha * sv[q];
+            uu[q] = mi[q] * r[q];                       // u = M^-1 r
+            const int u = tid + NT * q;
+            if (u < m) P_[u] = uu[q];
+        }
+        GLL_TRACE_CYC(11);
+        __syncthreads();
+        GLL_TRACE_CYC(12);
+        float gn = 0.f, de = -spmv(), rr = 0.f;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            spl[q] = spill(q);
+            gn += r[q] * uu[q];
+            de += dg[q] * uu[q] * uu[q] - uu[q] * spl[q];
+            rr += r[q] * r[q];
+        }
+#ifdef GLL_TRACE
+        if (it == 3 && blockIdx.x == 0 && threadIdx.x == 0 && de == 12345.f) g_trace[9] = 0;
+#endif
+        GLL_TRACE_CYC(13);
+        block_sum3<NT>(gn, de, rr, red, phase);
+        GLL_TRACE_CYC(14);
+        float w[R];
+        rowsums(w, spl);
+        if (rr <= tol2) {
+            conv = true;
+            break;
+        }
+        const float beta = gn * __builtin_amdgcn_rcpf(gam);
+        const float den = alpha * de - beta * gn;
+        if (!(den > 0.f)) break;   // breakdown or NaN: reported as non-converged
+        alpha = (gn * alpha) * __builtin_amdgcn_rcpf(den);
+        gam = gn;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            p[q] = uu[q] + beta * p[q];
+            sv[q] = w[q] + beta * sv[q];
+        }
+        GLL_TRACE_CYC(15);
+    }
+    GLL_TRACE_PT(8);
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int u = tid + NT * q;
+        if (u < m) {
+            if (out64) out64[size_t(u) * C + c] = double(x[q]);
+            if (out32) out32[size_t(u) * C + c] = x[q];
+        }
+    }
+    if (tid == 0) {
+        if (st_iters) atomicMax(st_iters, it);
+        if (!conv && st_nonconv) atomicAdd(st_nonconv, 1);
+    }
+}
+
 // Large systems: vectors in LDS (<= 160 KiB) or in the workspace.
 template <int NT, typename TB>
 __global__ __launch_bounds__(NT) void cg_lds_kernel(
@@ -758,6 +1064,27 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
     return launch_status("solve.hip:run_ell");
 }
 
+template <int NT, int R, int RV, typename TB>
+static hipError_t run_vr(const Layout& L, const Batch& bt, void* ws, const TB* b, size_t bs,
+                         double* out64, float* out32, float rtol, int max_iter,
+                         int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
+    if (L.m > NT * R || L.RV != RV || L.VRM <= 0 || L.VRM > 63) {   // row_build's packing
+        (void)hipGetLastError();
+        return hipErrorInvalidValue;
+    }
+    const size_t mp4 = size_t((L.m + 3) & ~3);
+    const size_t lds = 128 * 4 + mp4 * 4 + (size_t(NT) * RV + 4 * mp4) * 4 +
+                       size_t(NT) * RV * 4 + mp4 * 4;
+    auto fn = cg_vr_kernel<NT, R, RV, TB>;
+    allow_full_lds(reinterpret_cast<const void*>(fn));
+    launch_k(fn, dim3(L.C, bt.B), NT, lds, s,
+        L.m, L.C, L.base, L.VRM, L.at<int32_t>(ws, L.row_start), L.at<int32_t>(ws, L.row_len),
+        L.at<int32_t>(ws, L.ucnt), L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
+        L.at<float>(ws, L.diag), L.at<char>(ws, L.vr), b, out64, out32, rtol, max_iter,
+        st_nonconv, st_iters, bt.ws, bs, bt.u, bt.st);
+    return launch_status("solve.hip:run_vr");
+}
+
 template <typename TB>
 static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const TB* b, size_t bs,
                               double* out64, float* out32, float rtol, int max_iter,
@@ -786,6 +1113,17 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
                                           st_nonconv, st_iters, s)                          \
                : run_ell<NT, R, S, TB, 1>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
                                           st_nonconv, st_iters, s)
+    if (L.RV > 0) {   // the balanced kernel (row_build packed its virtual rows)
+#define GLL_VR(T_, R_, V_) \
+        if (L.RV == V_) return run_vr<T_, R_, V_, TB>(L, bt, ws, b, bs, out64, out32, rtol,   \
+                                                      max_iter, st_nonconv, st_iters, s)
+        if (m <= 512) { GLL_VR(512, 1, 4); GLL_VR(512, 1, 8); GLL_VR(512, 1, 10); }
+        if (m <= 1024) { GLL_VR(512, 2, 4); GLL_VR(512, 2, 8); GLL_VR(512, 2, 10); }
+        if (m <= 1536) { GLL_VR(512, 3, 4); GLL_VR(512, 3, 8); GLL_VR(512, 3, 10); }
+        GLL_VR(512, 4, 4); GLL_VR(512, 4, 8); GLL_VR(512, 4, 10);
+#undef GLL_VR
+        return hipErrorInvalidValue;
+    }
     if (m <= 64) GLL_ELL(64, 1, 24);
     if (m <= 128) GLL_ELL(128, 1, 24);
     if (m <= 256) GLL_ELL(256, 1, 24);

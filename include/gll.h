@@ -55,10 +55,15 @@ extern "C" {
 #define GLL_FLAG_GRAM_F32 16    /* retired in round 2 with the fp32-MFMA Gram kernels: rejected (GLL_ERR_UNSUPPORTED) */
 #define GLL_FLAG_CG_PIPE 32     /* per-column CG: pipelined PCG (one barrier per iteration) (diagnostic) */
 #define GLL_FLAG_GRAM_NOSPLIT 64 /* small single graphs: unsplit Gram tiles (one D2 plane) (diagnostic) */
-#define GLL_FLAG_DIAG_GRID_OVERSUB 128 /* tests: size the whole-GPU CG at twice its co-resident
-                                        * capacity -- the cooperative launch must be refused */
+#define GLL_FLAG_DIAG_GRID_OVERSUB 128 /* tests: size the whole-GPU CG at one row per workgroup,
+                                        * far past its co-resident capacity -- the cooperative
+                                        * launch must be refused */
 #define GLL_FLAG_DIAG_GRID_FAIL 256    /* tests: inject a grid-barrier failure into the
                                         * whole-GPU CG (NaN outputs + GLL_ST_SOLVE_FAILED) */
+#define GLL_FLAG_CG_ELL 512     /* per-column CG: register-ELL kernel even where the balanced
+                                 * (virtual-row) kernel would run (diagnostic) */
+#define GLL_FLAG_CG_VR 1024     /* per-column CG: balanced (virtual-row) kernel wherever it can
+                                 * run (m <= 2048) (diagnostic) */
 
 typedef struct gll_problem {
     int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */

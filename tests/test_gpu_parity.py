@@ -333,7 +333,8 @@ def _synth_batch(cfg, B, seed0=0):
 
 
 @pytest.mark.parametrize("cfg,eps,ydt,exact", [("plumbing", "auto", "i64", True),
-                                               ("ns", 1.0, "f32", False)])
+                                               ("ns", 1.0, "f32", False),
+                                               ("fullysup", 1.0, "f32", False)])
 def test_batched_graphs_equal_single_calls_bitwise(cfg, eps, ydt, exact):
     """B graphs in one launch per kernel give B single calls.  Bitwise where
     the batched launch runs the same CG configuration as the single one (plumbing); at NS
@@ -592,3 +593,45 @@ def test_grid_cg_past_capacity_falls_back_to_per_column(monkeypatch):
     ind = _gpu_knn(X, k, 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
     Uo, _ = O.forward(X, Y, tau=0.07, epsilon=1.0, K=k, knn=(ind, None))
     assert nc == 0 and O.rel_err(U, Uo) <= TOL
+
+
+@pytest.mark.parametrize("cfg,flags", [("fullysup", 0), ("ns", "vr"), ("plumbing", "vr")])
+def test_balanced_cg_matches_register_ell_and_oracle(cfg, flags):
+    """The balanced virtual-row CG (solve.hip cg_vr_kernel: the automatic choice at K = 25, the
+    FullySup shape; forced elsewhere) against the register-ELL kernel and the float64 oracle,
+    forward and adjoint (GLL.py:53,93)."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import CONFIGS, one_hot, synth
+    c = CONFIGS[cfg]
+    X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=2)
+    Y = one_hot(lab[: c["base"]])
+    fv = _lib.FLAG_CG_VR if flags == "vr" else 0
+    st_v, st_e = [], []
+    Uv, itv, ncv = _forward_c_abi(X, Y, c["k"], 0.07, 1.0, flags=fv, status=st_v)
+    Ue, ite, nce = _forward_c_abi(X, Y, c["k"], 0.07, 1.0, flags=_lib.FLAG_CG_ELL, status=st_e)
+    assert ncv == 0 and nce == 0 and 0 < itv <= ite + 2, (itv, ite)
+    ind = _gpu_knn(X, c["k"], 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, _ = O.forward(X, Y, tau=0.07, epsilon=1.0, K=c["k"], knn=(ind, None))
+    assert O.rel_err(Uv, Uo) <= TOL
+    assert O.rel_err(Uv, Ue) <= 1e-5
+
+
+def test_balanced_cg_spill_path_matches_oracle(monkeypatch):
+    """Virtual rows past the register capacity (forced to 4 per thread through GLL_VR_RV, so
+    most of the FullySup U block spills) are summed from the CSR by their rows' threads: same
+    answer, forward and adjoint, deterministic."""
+    from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth
+    c = CONFIGS["fullysup"]
+    X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=4)
+    Y = one_hot(lab[: c["base"]])
+    g = seeded_gbar(c["batch"], 10, 9)
+    monkeypatch.setenv("GLL_VR_RV", "4")
+    U1, gr1 = _run(X, Y, 0.07, 1.0, c["k"], g)
+    U2, gr2 = _run(X, Y, 0.07, 1.0, c["k"], g)
+    monkeypatch.delenv("GLL_VR_RV")
+    np.testing.assert_array_equal(U1, U2)
+    np.testing.assert_array_equal(gr1, gr2)
+    ind = _gpu_knn(X, c["k"], 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, st = O.forward(X, Y, tau=0.07, epsilon=1.0, K=c["k"], knn=(ind, None))
+    assert O.rel_err(U1, Uo) <= TOL
+    assert O.rel_err(gr1, O.backward(st, g)) <= TOL

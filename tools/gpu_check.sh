@@ -40,6 +40,10 @@ fi
 if [[ $STEPS == *host* ]]; then
   run host 300 python tools/host_overhead.py
 fi
+if [[ $STEPS == *mfmalist* ]]; then
+  run counters_list 120 rocprofv3 -L
+  grep -oE "(SQ_[A-Z_]*MFMA[A-Z0-9_]*|GRBM_GUI_ACTIVE|SQ_BUSY_CYCLES|SQ_WAVE_CYCLES)" gpurun_out/counters_list.log | sort -u | head -40
+fi
 if [[ $STEPS == *ctr* ]]; then
   export TMPDIR=/tmp
   R=$PWD

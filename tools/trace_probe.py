@@ -18,7 +18,10 @@ from graphlearninglayer_amd import GLL, _lib  # noqa: E402
 from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth  # noqa: E402
 
 TICK_US = 0.01
-lib = ct.CDLL(os.path.join(ROOT, "graphlearninglayer_amd", "_obj", "libgll_trace.so"))
+# _obj/ stays on this side (.gpurunignore): copy the trace build next to this script to ship it
+_tl = os.path.join(ROOT, "tools", "libgll_trace.so")
+lib = ct.CDLL(_tl if os.path.exists(_tl) else
+              os.path.join(ROOT, "graphlearninglayer_amd", "_obj", "libgll_trace.so"))
 lib.gll_workspace_bytes.restype = ct.c_size_t
 lib.gll_trace_read.argtypes = [ct.c_int, ct.POINTER(ct.c_ulonglong)]
 UNITS = {0: ("knn", ["gram", "select", "gram_wide", "gram48", "gram_bf3"]), 1: ("rows", ["row_build"]),
@@ -35,7 +38,7 @@ X_np, lab = synth(base, n - base, d, r=c["r"], seed=0)
 X = torch.from_numpy(X_np).to(dev)
 Y = torch.from_numpy(one_hot(lab[:base])).to(dev)
 g = torch.from_numpy(seeded_gbar(n - base, 10)).to(dev)
-prob = GLL.make_problem(n, d, base, 10, k, 0.07, eps)
+prob = GLL.make_problem(n, d, base, 10, k, 0.07, eps, flags=int(os.environ.get("TRACE_FLAGS", "0")))
 ws = torch.empty(lib.gll_workspace_bytes(ct.byref(prob)), dtype=torch.uint8, device=dev)
 U = torch.empty(n - base, 10, dtype=torch.float64, device=dev)
 gx = torch.empty(n, d, dtype=torch.float32, device=dev)
