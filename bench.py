@@ -136,6 +136,34 @@ def pmc_traffic(config, kernel):
     return None
 
 
+def _newest_profile(pattern):
+    import glob
+    here = os.path.dirname(os.path.abspath(__file__))
+    paths = sorted(glob.glob(os.path.join(here, "profiles", pattern)))
+    return os.path.join("profiles", os.path.basename(paths[-1])) if paths else None
+
+
+def gram_mfma_pmc(config):
+    """The Gram's MFMA counters from the newest committed summary (profiles/rNN_mfma_<config>.json,
+    tools/mfma_summary.py over a rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16
+    SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE pass), or None."""
+    import glob
+    here = os.path.dirname(os.path.abspath(__file__))
+    paths = sorted(glob.glob(os.path.join(here, "profiles", f"r*_mfma_{config}.json")))
+    if not paths:
+        return None
+    with open(paths[-1]) as f:
+        doc = json.load(f)
+    for sym in PMC_SYMBOLS["gram_d2_kernel"]:
+        e = doc["kernels"].get(sym)
+        if e and "exec_bf16_tflops" in e:
+            return {"kernel": sym, "exec_bf16_tflops": e["exec_bf16_tflops"],
+                    "exec_frac_of_bf16_peak": e["exec_flops_frac_of_peak"],
+                    "mfma_busy_frac": e.get("mfma_busy_frac"), "duration_us": e["duration_us"],
+                    "source": os.path.join("profiles", os.path.basename(paths[-1]))}
+    return None
+
+
 def batched_measure(c, eps, tau, k, B, units, dev, rank, steps=20, warmup=5):
     """B independent graphs of the workload per call of the batched entry point (X: B x n x d):
     whole-batch fwd+bwd throughput, and the CG kernel against the HBM roofline, where one
@@ -179,7 +207,10 @@ def batched_measure(c, eps, tau, k, B, units, dev, rank, steps=20, warmup=5):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "work_per_launch": B * work, "avg_launch_us": round(avg_s * 1e6, 3),
-                         "launches": cnt}}
+                         "launches": cnt,
+                         "traffic": pmc_traffic(f"{c['name']}_b{B}", "cg_kernel"),
+                         "rocprof_stats": _newest_profile(f"*_{c['name']}_b{B}_kernel_stats.csv")},
+            "gram_mfma_pmc": gram_mfma_pmc(f"{c['name']}_b{B}")}
 
 
 def c_abi_measure(X, Y, tau, eps, k, gbar, steps, warmup):
@@ -358,6 +389,7 @@ def main():
 
     c = dict(CONFIGS[a.config])
     c["n"] = c["base"] + c["batch"]
+    c["name"] = a.config
     eps, tau, k = EPS[a.config], TAU[a.config], c["k"]
     X_np, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=shard_rank_seed(0, rank))
     X = torch.from_numpy(X_np).to(dev).requires_grad_(True)
@@ -451,7 +483,8 @@ def main():
                     "peak": peak, "unit": unit, "frac": round(achieved / peak, 5),
                     "traffic": pmc_traffic(a.config, dominant), "work_per_launch": work,
                     "avg_launch_us": round(avg_s * 1e6, 3), "launches": cnt,
-                    "cg_iters_fwd_bwd": list(iters)}
+                    "cg_iters_fwd_bwd": list(iters),
+                    "gram_mfma_pmc": gram_mfma_pmc(a.config)}
         # whole-call roofline: kNN at its MFMA roof + every other byte at HBM
         f_knn = units["gram_d2_kernel"][1]
         b_rest = sum(w_ * per_kernel[kn]["launches_per_step"] for kn, (b_, w_) in units.items()
