@@ -116,7 +116,7 @@ PMC_SYMBOLS = {"gram_d2_kernel": ["gram_bf3s_kernel", "gram_bf3_kernel", "gram_b
                                    "gram_lds_kernel", "gram_wide_kernel"], "knn_select_kernel": ["knn_select_kernel"],
                "row_build_kernel": ["row_build_kernel"],
                "cg_kernel": ["cg_ell_kernel", "cg_vr_kernel", "cg_grid_kernel", "cg_lds_kernel"],
-               "edge_coef_kernel": ["edge_coef_kernel"], "grad_spmm_kernel": ["grad_spmm_kernel"]}
+               "edge_coef_kernel": ["edge_coef_kernel"], "grad_spmm_kernel": ["grad_spmm_kernel", "grad_chunk_kernel"]}
 
 
 def pmc_traffic(config, kernel):

@@ -199,7 +199,7 @@ struct Layout {
         vr = take(size_t(m) * VRM * kVrSlot);
         P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)
         Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
-        S = take(size_t(Etot) * 4);        // per-edge coefficient (auto eps only)
+        S = take(size_t(Etot) * 4);        // per-edge coefficient (auto eps / chunked gradient)
         b = take(size_t(n) * 4);           // auto-eps b_i (GLL.py:126)
         // CG vectors when they do not fit in LDS (per-column kernels) / of the grid-wide CG
         const size_t gf = grid_cg_workspace_floats(m, C);

@@ -64,7 +64,7 @@ __device__ __forceinline__ float edge_gv(const EdgeArgs& a, int i, int j, float 
     return g * v;
 }
 
-// auto eps, pass 1: S_ij and b_i
+// auto eps, pass 1: S_ij and b_i (also the fixed-eps S_ij of the feature-chunked gradient)
 __global__ __launch_bounds__(256) void edge_coef_kernel(EdgeArgs a) {
     GLL_TRACE_SCOPE(0);
     a.to_graph();
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void edge_coef_kernel(EdgeArgs a) {
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
     const int beg = a.row_start[i], end = beg + a.row_len[i];
-    const float ei = a.eps[i];
+    const float ei = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[i];
     float bpart = 0.f;
     for (int e = beg + lane; e < end; e += kWave) {
         float g;
@@ -172,6 +172,112 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
     }
 }
 
+// Feature-chunked form: the same sums with the features split into NCH chunks of 4 LPR floats,
+// block b taking chunk b % NCH.  Blocks are dealt round-robin over the 8 XCDs, so with NCH | 8
+// each XCD gathers only its own chunk of the neighbour rows: its working set is n x d / NCH x 4 B
+// (4 MB at stress, d = 1024, NCH = 8), which its L2 holds, instead of all of X (32 MB) streamed
+// from the MALL once per edge.  LPR lanes own one row (RPW = 64 / LPR rows per wave): they first
+// own the row's edges (coefficients), then its chunk's feature columns; an edge's coefficient and
+// column reach the group's lanes by a width-LPR shuffle.  The per-edge coefficient is recomputed
+// per chunk (C-wide gathers from the n x C arrays, L2-resident).  Same edge order and summation
+// per element as grad_spmm_kernel, so the two agree bitwise.
+// COEF: 0 = fixed eps, coefficient G V per edge inline; 1 = auto eps (S and b from
+// edge_coef_kernel); 2 = fixed eps, S from edge_coef_kernel (the inline form would be recomputed
+// by every chunk: 4 C gathers per edge, which at NCH = 8 cost more than the chunking saves).
+template <int COEF, int LPR>
+__global__ __launch_bounds__(256) void grad_chunk_kernel(EdgeArgs a, const float* __restrict__ X,
+                                                         float* __restrict__ out, int nch,
+                                                         size_t xs, size_t gxs) {
+    GLL_TRACE_SCOPE(1);
+    a.to_graph();
+    X = gshift(X, xs);
+    out = gshift(out, gxs);
+    constexpr int RPW = kWave / LPR;
+    constexpr int EB = LPR >= 32 ? 8 : 16;   // neighbour rows in flight per lane
+    const int lane = lane_id();
+    const int gl = lane % LPR;                // lane inside the row's group
+    const int chunk = blockIdx.x % nch;
+    const int i = (blockIdx.x / nch) * (4 * RPW) + (threadIdx.x >> 6) * RPW + lane / LPR;
+    const bool live = i < a.n;
+    const int ic = live ? i : 0;
+    const int d = a.d;
+    const int k = chunk * 4 * LPR + 4 * gl;   // this lane's 4 features
+    const bool kin = k < d;
+    const int kc = kin ? k : 0;
+    const int beg = live ? a.row_start[ic] : 0;
+    const int end = live ? beg + a.row_len[ic] : 0;
+    const float ei = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[ic];
+    const f32x4 xv = *reinterpret_cast<const f32x4*>(X + size_t(ic) * d + kc);
+    int kth_i = 0;
+    float b_i = 0.f;
+    if constexpr (COEF == 1) {
+        kth_i = a.knn_idx[size_t(ic) * a.K + a.K - 1];
+        b_i = a.b[ic];
+    }
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int e0 = beg; e0 < end; e0 += LPR) {
+        const int e = e0 + gl;
+        float cf = 0.f;
+        int cj = ic;
+        if (e < end) {
+            cj = a.col[e];
+            if constexpr (COEF == 1) {
+                cf = a.S[e];
+                if (cj == kth_i) cf -= b_i;
+                if (a.knn_idx[size_t(cj) * a.K + a.K - 1] == i) cf -= a.b[cj];
+            } else if constexpr (COEF == 2) {
+                cf = a.S[e];
+            } else {
+                float g;
+                cf = edge_gv(a, ic, cj, a.w[e], ei, g);
+            }
+        }
+        const int cnt = min(LPR, end - e0);
+        for (int t0 = 0; t0 < cnt; t0 += EB) {
+            float s[EB];
+            f32x4 v[EB];
+#pragma unroll
+            for (int u = 0; u < EB; ++u) {
+                const int t = t0 + u < cnt ? t0 + u : t0;
+                s[u] = __shfl(cf, t, LPR);
+                s[u] = t0 + u < cnt ? s[u] : 0.f;
+                const int j = __shfl(cj, t, LPR);
+                v[u] = *reinterpret_cast<const f32x4*>(X + size_t(j) * d + kc);
+            }
+#pragma unroll
+            for (int u = 0; u < EB; ++u) acc += s[u] * (xv - v[u]);
+        }
+    }
+    if (live && kin)
+        __builtin_nontemporal_store(acc, reinterpret_cast<f32x4*>(out + size_t(i) * d + k));
+}
+
+// Whether the feature-chunked gradient runs: 16-B rows with d >= 128, and a graph whose X does
+// not fit an XCD's 4 MB L2 (measured, tools/ab_flags.py --flags 2048,4096: stress grad 192 ->
+// 94 us; NS 8.7 -> 13.7 us and B = 64 NS 197 -> 527 us, where X already fits and the chunks
+// only multiply the per-edge work), or forced by the flags.
+static bool grad_use_chunks(const Layout& L, bool vec) {
+    if (!vec || L.d < 128 || (L.d & 3) || (L.flags & GLL_FLAG_GRAD_ROWS)) return false;
+    return (L.flags & GLL_FLAG_GRAD_CHUNK) || size_t(L.n) * L.d * 4 > (size_t(4) << 20);
+}
+
+// LPR = the power of two nearest d / 32 in [16, 64], NCH = ceil(d / (4 LPR)) chunks.
+template <int COEF>
+static void grad_chunked(const EdgeArgs& a, const Batch& bt, const float* X, float* out,
+                         hipStream_t s) {
+    int lpr = 16;
+    while (lpr < 64 && 4 * lpr * 8 < a.d) lpr *= 2;
+    const int nch = (a.d + 4 * lpr - 1) / (4 * lpr);
+    const int rows_per_block = 4 * (kWave / lpr);
+    dim3 grid(unsigned(nch * ((a.n + rows_per_block - 1) / rows_per_block)), bt.B);
+    if (lpr == 16)
+        launch_k(grad_chunk_kernel<COEF, 16>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx);
+    else if (lpr == 32)
+        launch_k(grad_chunk_kernel<COEF, 32>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx);
+    else
+        launch_k(grad_chunk_kernel<COEF, 64>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx);
+}
+
 template <bool AUTO, bool VEC>
 static hipError_t grad_nd(const EdgeArgs& a, const Batch& bt, const float* X, float* out,
                           hipStream_t s) {
@@ -217,20 +323,26 @@ hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, cons
     a.b = L.at<float>(ws, L.b);
     a.wss = bt.ws;
     hipError_t e;
-    if (auto_eps) {
+    const bool chunk = grad_use_chunks(L, vec);
+    if (auto_eps || chunk) {   // per-edge S (and b) first
         prof_begin(GLL_K_EDGE, s);
         launch_k(edge_coef_kernel, dim3((L.n + 3) / 4, bt.B), 256, 0, s, a);
         prof_end(GLL_K_EDGE, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        prof_begin(GLL_K_GRAD, s);
-        e = vec ? grad_nd<true, true>(a, bt, X, gradX, s) : grad_nd<true, false>(a, bt, X, gradX, s);
-        prof_end(GLL_K_GRAD, s);
+    }
+    prof_begin(GLL_K_GRAD, s);
+    if (chunk) {
+        if (auto_eps) grad_chunked<1>(a, bt, X, gradX, s);
+        else grad_chunked<2>(a, bt, X, gradX, s);
+        e = launch_status("grad.hip:grad_chunked");
+    } else if (auto_eps) {
+        e = vec ? grad_nd<true, true>(a, bt, X, gradX, s)
+                : grad_nd<true, false>(a, bt, X, gradX, s);
     } else {
-        prof_begin(GLL_K_GRAD, s);
         e = vec ? grad_nd<false, true>(a, bt, X, gradX, s)
                 : grad_nd<false, false>(a, bt, X, gradX, s);
-        prof_end(GLL_K_GRAD, s);
     }
+    prof_end(GLL_K_GRAD, s);
     return e;
 }
 

@@ -64,6 +64,10 @@ extern "C" {
                                  * (virtual-row) kernel would run (diagnostic) */
 #define GLL_FLAG_CG_VR 1024     /* per-column CG: balanced (virtual-row) kernel wherever it can
                                  * run (m <= 2048) (diagnostic) */
+#define GLL_FLAG_GRAD_ROWS 2048 /* feature gradient: whole-row kernel even where the
+                                 * feature-chunked one would run (diagnostic) */
+#define GLL_FLAG_GRAD_CHUNK 4096 /* feature gradient: feature-chunked kernel wherever it can
+                                  * run (d >= 128, d % 4 == 0) (diagnostic) */
 
 typedef struct gll_problem {
     int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */
