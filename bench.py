@@ -112,7 +112,7 @@ def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps):
 
 
 # C-ABI kernel ids (gll_kernel_name) -> device symbols as rocprofv3 names them
-PMC_SYMBOLS = {"gram_d2_kernel": ["gram_bf3s_kernel", "gram_bf3_kernel", "gram_bf3w_kernel", "gram48_kernel",
+PMC_SYMBOLS = {"gram_d2_kernel": ["gram_pk_kernel", "gram_bf3s_kernel", "gram_bf3_kernel", "gram_bf3w_kernel", "gram48_kernel",
                                    "gram_lds_kernel", "gram_wide_kernel"], "knn_select_kernel": ["knn_select_kernel"],
                "row_build_kernel": ["row_build_kernel"],
                "cg_kernel": ["cg_ell_kernel", "cg_vr_kernel", "cg_grid_kernel", "cg_lds_kernel"],

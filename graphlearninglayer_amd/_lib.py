@@ -27,6 +27,7 @@ FLAG_CG_ELL = 512   # gll_problem.flags: register-ELL per-column CG where the ba
 FLAG_CG_VR = 1024   # gll_problem.flags: balanced (virtual-row) per-column CG wherever it fits
 FLAG_GRAD_ROWS = 2048   # gll_problem.flags: whole-row feature-gradient kernel (diagnostic)
 FLAG_GRAD_CHUNK = 4096  # gll_problem.flags: feature-chunked gradient kernel wherever it runs
+FLAG_GRAM_INLINE = 8192  # gll_problem.flags: 128-tile Gram with the inline split (diagnostic)
 ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
 ST_KNN_RESCAN = 5   # kNN rows re-ranked over every column under the Gram error bound
 ST_SOLVE_FAILED = 6   # a whole-GPU CG lost a grid barrier: outputs NaN, raised as an error

@@ -154,6 +154,8 @@ struct Layout {
     int RV;           // balanced CG: virtual rows per thread (vr_threads), 0 = not used
     int VRM;          // balanced CG: virtual-row slots per U row (vr_max_per_row)
     size_t vr;        // [m][VRM] packed virtual rows (kVrSlot bytes each)
+    int dp;           // split-Gram planes: d rounded up to 64
+    size_t xhi, xlo, xnrm;   // [n][dp] bf16 hi / lo planes of x - x_0, and |x - x_0|^2
 
     explicit Layout(const gll_problem& p) {
         n = p.n; d = p.d; base = p.base; C = p.C;
@@ -197,6 +199,10 @@ struct Layout {
         RV = vr_threads(n, m, K, flags);
         VRM = RV ? vr_max_per_row(K) : 0;
         vr = take(size_t(m) * VRM * kVrSlot);
+        dp = (d + 63) & ~63;
+        xhi = take(size_t(n) * dp * 2);
+        xlo = take(size_t(n) * dp * 2);
+        xnrm = take(size_t(n) * 4);
         P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)
         Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
         S = take(size_t(Etot) * 4);        // per-edge coefficient (auto eps / chunked gradient)
@@ -404,14 +410,27 @@ hipError_t launch_status(const char* what);
 struct ArmedLaunch {
     int kid = -1;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    int span = 1;   // launches the timed phase spans: the first records e0, the last e1
 };
 extern thread_local ArmedLaunch g_armed;
 
+// A timed phase made of `n` consecutive launches (e.g. the Gram's split + GEMM): call right
+// after prof_begin.
+inline void prof_span(int n) {
+    if (g_armed.kid >= 0) g_armed.span = n;
+}
+
 template <typename F, typename... Args>
 inline void launch_k(F fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, Args... args) {
-    if (g_armed.kid >= 0) {
+    if (g_armed.kid >= 0 && g_armed.span > 1) {
+        const hipEvent_t e0 = g_armed.e0;
+        g_armed.e0 = nullptr;
+        --g_armed.span;
+        hipExtLaunchKernelGGL(fn, grid, block, uint32_t(lds), s, e0, nullptr, 0u, args...);
+    } else if (g_armed.kid >= 0) {
         const hipEvent_t e0 = g_armed.e0, e1 = g_armed.e1;
         g_armed.kid = -1;
+        g_armed.span = 1;
         hipExtLaunchKernelGGL(fn, grid, block, uint32_t(lds), s, e0, e1, 0u, args...);
     } else {
         fn<<<grid, block, lds, s>>>(args...);

@@ -567,6 +567,225 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
 }
 
 // --------------------------------------------------------------------------------------
+// K1a (large problems and batches, round 2): the split done once per row, then a bf16 GEMM.
+//
+// gram_split_kernel: a_i = x_i - x_0 (centred on row 0 as above), hi = bf16(a), lo = bf16(a -
+// hi) into two [n][dp] bf16 planes (dp = d rounded up to 64, zero-padded) and |a_i|^2 (fp32)
+// into nrm[n]: one pass over X.  gram_bf3w_kernel redid this split for every tile a row takes
+// part in (T times), on the VALU between two barriers per 128-feature phase.
+//
+// gram_pk_kernel: 128 x 128 upper-triangle tiles (same tile list and XCD order as bf3w), 4
+// waves of 64 x 64 (2 x 2 accumulators of 32 x 32), k-stages of 64 features: the four tile
+// planes (A hi, A lo, B hi, B lo; 64 KiB) go global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, no VGPR staging, no conversion), double-buffered so stage k+1's
+// loads are in flight while stage k's 48 MFMAs per wave run.  Rows are 128 B in LDS with the
+// 16-B segments XOR-swizzled by (row >> 1) & 7 -- on the SOURCE address, the DMA writes
+// lane-linearly -- so the ds_read_b128 fragment reads of 16 consecutive rows hit 16 distinct
+// bank groups.  The stage wait is a counted vmcnt (this wave's 16 DMAs of the older stage) and
+// a raw s_barrier, so the prefetch stays in flight across it (cdna_hip_programming.md
+// "Pipelining across barriers").
+// --------------------------------------------------------------------------------------
+constexpr int kPK = 64;                  // features per k-stage
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict__ X, int n, int d,
+                                                         int dp, __bf16* __restrict__ Ph,
+                                                         __bf16* __restrict__ Pl,
+                                                         float* __restrict__ nrm,
+                                                         int32_t* __restrict__ status,
+                                                         int32_t* __restrict__ rev_cnt,
+                                                         size_t xs, size_t wss) {
+    X = gshift_br(X, xs);
+    Ph = gshift_br(Ph, wss);
+    Pl = gshift_br(Pl, wss);
+    nrm = gshift_br(nrm, wss);
+    status = gshift_br(status, wss);
+    rev_cnt = gshift_br(rev_cnt, wss);
+    {   // per-call reset of the counters the select kernel accumulates into
+        const int g = blockIdx.x * 256 + threadIdx.x;
+        if (g < GLL_ST_NWORDS) status[g] = 0;
+        for (int q = g; q < n; q += gridDim.x * 256) rev_cnt[q] = 0;
+    }
+    const int lane = lane_id();
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const float* xi = X + size_t(i) * d;
+    float sq = 0.f;
+    for (int k = 4 * lane; k < dp; k += 4 * kWave) {
+        const f32x4 c = load4<VEC>(X, k, d);
+        const f32x4 f = load4<VEC>(xi, k, d) - c;   // zeros past d
+        sq += f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+        bf16x4 hv, lv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const __bf16 hb = static_cast<__bf16>(f[e]);
+            hv[e] = hb;
+            lv[e] = static_cast<__bf16>(f[e] - static_cast<float>(hb));
+        }
+        *reinterpret_cast<bf16x4*>(Ph + size_t(i) * dp + k) = hv;
+        *reinterpret_cast<bf16x4*>(Pl + size_t(i) * dp + k) = lv;
+    }
+    sq = wave_sum_dpp(sq);
+    if (lane == 0) nrm[i] = sq;
+}
+
+__global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__ Ph,
+                                                      const __bf16* __restrict__ Pl,
+                                                      const float* __restrict__ nrm, int n,
+                                                      int dp, int T, float* __restrict__ D2,
+                                                      int ld, size_t wss) {
+    Ph = gshift_br(Ph, wss);
+    Pl = gshift_br(Pl, wss);
+    nrm = gshift_br(nrm, wss);
+    D2 = gshift_br(D2, wss);
+    constexpr int kTP = 128 * kPK;                                  // bf16 per tile plane
+    __shared__ __attribute__((aligned(16))) __bf16 sm[2 * 4 * kTP];  // 128 KiB: [buf][plane]
+    const int lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    int bi = 0, rem = xcd_tile(blockIdx.x, gridDim.x);
+    while (rem >= T - bi) {
+        rem -= T - bi;
+        ++bi;
+    }
+    const int bj = bi + rem;
+    const int wr = w >> 1, wc = w & 1;
+    // this lane's DMA sources: 16 per stage = plane q >> 2, rows 8 c .. 8 c + 7 (c = (q & 3) 4 + w)
+    // as 1 KiB pieces; lane -> row 8 c + lane / 8, LDS segment lane % 8 <- source segment
+    // (lane % 8) ^ ((row >> 1) & 7)
+    const __bf16* src[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int pl = q >> 2, c = (q & 3) * 4 + w;
+        const int row = 8 * c + (lane >> 3);
+        const int seg = (lane & 7) ^ ((row >> 1) & 7);
+        int grow = (pl < 2 ? bi : bj) * 128 + row;
+        grow = grow < n ? grow : n - 1;
+        src[q] = ((pl & 1) ? Pl : Ph) + size_t(grow) * dp + 8 * seg;
+    }
+    auto issue = [&](int ks, int buf) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int pl = q >> 2, c = (q & 3) * 4 + w;
+            __bf16* dst = sm + (buf * 4 + pl) * kTP + c * 8 * kPK;
+            __builtin_amdgcn_global_load_lds(src[q] + ks * kPK, (lds_void*)dst, 16, 0, 0);
+        }
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+    auto frag = [&](int buf, int pl, int row, int kk) {
+        const int pos = (2 * kk + h) ^ ((row >> 1) & 7);
+        return *reinterpret_cast<const bf16x8*>(sm + (buf * 4 + pl) * kTP + row * kPK + 8 * pos);
+    };
+    const int nks = dp / kPK;
+    issue(0, 0);
+    for (int ks = 0; ks < nks; ++ks) {
+        const int buf = ks & 1;
+        if (ks + 1 < nks) {
+            issue(ks + 1, buf ^ 1);
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // this wave's stage-ks DMAs
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();                          // every wave's stage-ks DMAs
+#pragma unroll
+        for (int kk = 0; kk < kPK / 16; ++kk) {
+            bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                ah[m] = frag(buf, 0, wr * 64 + m * 32 + r, kk);
+                al[m] = frag(buf, 1, wr * 64 + m * 32 + r, kk);
+                bh[m] = frag(buf, 2, wc * 64 + m * 32 + r, kk);
+                bl[m] = frag(buf, 3, wc * 64 + m * 32 + r, kk);
+            }
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+                }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();   // buffer `buf` is refilled by the next stage's DMAs
+    }
+    // epilogue: D2 = |a_i|^2 + |a_j|^2 - 2 <a_i, a_j>; C layout of 32x32: col = lane & 31,
+    // row = (e & 3) + 8 (e >> 2) + 4 h
+    float nj[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int j = bj * 128 + wc * 64 + b * 32 + r;
+        nj[b] = nrm[j < n ? j : n - 1];
+    }
+    if (bi != bj) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const int i0 = bi * 128 + wr * 64 + a * 32;
+            float ni[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int i = i0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                ni[e] = nrm[i < n ? i : n - 1];
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int j = bj * 128 + wc * 64 + b * 32 + r;
+                float dv[16];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) dv[e] = ni[e] + nj[b] - 2.f * acc[a][b][e];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {   // direct: 32 lanes per 128-B row piece
+                    const int i = i0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    if (i < n && j < n) D2[size_t(i) * ld + j] = dv[e];
+                }
+                if (j < n) {   // mirrored: row j, columns i0 + 8 g + 4 h .. +3
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int i = i0 + 8 * g + 4 * h;
+                        float* dst = D2 + size_t(j) * ld + i;
+                        if (i + 4 <= n) {
+                            *reinterpret_cast<f32x4*>(dst) =
+                                f32x4{dv[4 * g], dv[4 * g + 1], dv[4 * g + 2], dv[4 * g + 3]};
+                        } else {
+#pragma unroll
+                            for (int t = 0; t < 4; ++t)
+                                if (i + t < n) dst[t] = dv[4 * g + t];
+                        }
+                    }
+                }
+            }
+        }
+    } else {
+        // diagonal tile: stage [128][129] in LDS, store the upper triangle in both orientations
+        float* tile = reinterpret_cast<float*>(sm);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int ti = wr * 64 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    const int tj = wc * 64 + b * 32 + r;
+                    const int i = bi * 128 + ti;
+                    tile[ti * 129 + tj] = nrm[i < n ? i : n - 1] + nj[b] - 2.f * acc[a][b][e];
+                }
+        __syncthreads();
+        for (int q = threadIdx.x; q < 128 * 128; q += 256) {
+            const int ti = q >> 7, tj = q & 127;
+            const int i = bi * 128 + ti, j = bi * 128 + tj;
+            if (i < n && j < n) D2[size_t(i) * ld + j] = tj >= ti ? tile[ti * 129 + tj] : tile[tj * 129 + ti];
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------------
 // K1b: per-row selection + exact re-rank + reverse scatter
 // --------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t pack_key(float d2, int j) {
@@ -1130,6 +1349,24 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
     // 128-tiles when there are enough of them to fill the chip twice (large graphs and batches;
     // a single NS graph has only 36); 64-tiles otherwise
     const int T = (L.n + 127) / 128;
+    if (!(L.flags & GLL_FLAG_GRAM_NARROW) && int64_t(bt.B) * T * (T + 1) / 2 >= 512 &&
+        !(L.flags & GLL_FLAG_GRAM_INLINE)) {
+        // split once (one pass over X), then the LDS-DMA bf16 GEMM over 128-tiles
+        __bf16* Ph = L.at<__bf16>(ws, L.xhi);
+        __bf16* Pl = L.at<__bf16>(ws, L.xlo);
+        float* nrm = L.at<float>(ws, L.xnrm);
+        prof_begin(GLL_K_GRAM, s);
+        prof_span(2);
+        const dim3 sgrid((L.n + 3) / 4, bt.B);
+        if (vec)
+            launch_k(gram_split_kernel<true>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
+        else
+            launch_k(gram_split_kernel<false>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
+        launch_k(gram_pk_kernel, dim3(T * (T + 1) / 2, bt.B), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T,
+                 D2, L.ldD, bt.ws);
+        prof_end(GLL_K_GRAM, s);
+        return launch_status("knn.hip:launch_gram(pk)");
+    }
     if (!(L.flags & GLL_FLAG_GRAM_NARROW) && int64_t(bt.B) * T * (T + 1) / 2 >= 512) {
         const dim3 grid(T * (T + 1) / 2, bt.B);
         prof_begin(GLL_K_GRAM, s);

@@ -68,6 +68,8 @@ extern "C" {
                                  * feature-chunked one would run (diagnostic) */
 #define GLL_FLAG_GRAD_CHUNK 4096 /* feature gradient: feature-chunked kernel wherever it can
                                   * run (d >= 128, d % 4 == 0) (diagnostic) */
+#define GLL_FLAG_GRAM_INLINE 8192 /* 128-tile Gram: split each tile's rows inline (the round-1
+                                   * kernel) instead of pre-split planes + LDS-DMA (diagnostic) */
 
 typedef struct gll_problem {
     int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */

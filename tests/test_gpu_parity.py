@@ -684,3 +684,23 @@ def test_chunked_grad_matches_row_kernel_bitwise(cfg, eps):
     ind = _gpu_knn(X, c["k"], eps)["knn_idx"].cpu().numpy().astype(np.int64)
     Uo, st = O.forward(X, Y, tau=0.07, epsilon=eps, K=c["k"], knn=(ind, None))
     assert O.rel_err(gc, O.backward(st, g)) <= TOL
+
+
+@pytest.mark.parametrize("d", [100, 37, 256])
+def test_presplit_gram_matches_inline_split(d):
+    """The 128-tile Gram on pre-split hi/lo planes with LDS-DMA staging (knn.hip gram_split_kernel
+    + gram_pk_kernel, the default for large graphs and batches) against the inline-split kernel
+    (GLL_FLAG_GRAM_INLINE): both only nominate candidates, so the kNN (exact against float64)
+    and every output agree bitwise; ragged n (not a multiple of 128) and d (not of 64, and not
+    of 4: the scalar load path)."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import one_hot, synth
+    base, m, k = 1000, 3037, 10   # 32 128-row tiles a side: 528 tiles, the 128-tile path
+    X, lab = synth(base, m, d, r=1.0, seed=8)
+    Y = one_hot(lab[:base])
+    Up, itp, ncp = _forward_c_abi(X, Y, k, 0.07, "auto")
+    Ui, iti, nci = _forward_c_abi(X, Y, k, 0.07, "auto", flags=_lib.FLAG_GRAM_INLINE)
+    assert ncp == 0 and nci == 0
+    np.testing.assert_array_equal(Up, Ui)
+    ind = _gpu_knn(X, k, "auto")["knn_idx"].cpu().numpy()
+    assert _exact_knn_rows(X, ind, k) == []
