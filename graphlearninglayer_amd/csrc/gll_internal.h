@@ -381,23 +381,48 @@ struct Batch {
     size_t st = 0;   // public status words: ws when they live in the workspace, 0 for a sink
 };
 
+// XCD-aware block numbering of batched launches.  Blocks are dealt round-robin over the 8 XCDs
+// in dispatch order (linear index L = y * gridDim.x + x, XCD = L % 8; MI355X_MICROARCH.md: a
+// speed assumption, never a correctness one).  For gridDim.y = B > 1 graphs, block (x, y) is
+// renumbered so that each XCD works through a contiguous run of the graph-major sequence: a
+// graph's blocks share one XCD's L2 (its X rows, its D2, its CSR) instead of each of the 8
+// XCDs refilling every graph.  batch_xy() = (block within the graph, graph); single graphs keep
+// (blockIdx.x, 0).  Every kernel that runs batched takes its block and graph from here.
+template <bool R = false>
+__device__ __forceinline__ int2 batch_xy() {
+    if (!R || gridDim.y == 1) return int2{int(blockIdx.x), int(blockIdx.y)};
+    const int nb = gridDim.x, nt = nb * gridDim.y;
+    const int L = blockIdx.y * nb + blockIdx.x;
+    const int x = L & 7, q = L >> 3, per = nt >> 3, extra = nt & 7;
+    const int idx = x * per + (x < extra ? x : extra) + q;
+    return int2{idx % nb, idx / nb};
+}
+// R = true only where it measured faster (tools/ab_flags.py, B = 64 / 8): the per-column CG
+// (NS B = 64 32 -> 24 us, stress B = 64 2.0 -> 1.1 ms) and the whole-row feature gradient (NS
+// B = 64 198 -> 178 us, FullySup B = 64 347 -> 305 us).  Row build (NS B = 64 60 -> 170 us) and
+// select (251 -> 292 us) ran slower with it, and the chunked gradient needs block % 8 = chunk.
+template <bool R = false>
+__device__ __forceinline__ int bx() { return batch_xy<R>().x; }
+template <bool R = false>
+__device__ __forceinline__ int bg() { return batch_xy<R>().y; }
+
 // Branch-free on purpose: a branch per pointer splits the prologue into basic blocks with an
 // s_waitcnt each, serialising the kernel-argument loads (~13 dependent scalar loads, ~0.5 us
 // at the start of every kernel); selects let them all be in flight at once.
-template <typename T>
+template <bool R = false, typename T>
 __device__ __forceinline__ T* gshift(T* p, size_t stride) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uintptr_t off = uintptr_t(blockIdx.y) * stride;
+    const uintptr_t off = uintptr_t(bg<R>()) * stride;
     return reinterpret_cast<T*>(a + (a != 0 ? off : uintptr_t(0)));
 }
 
 // Branching form for the register-tight Gram kernels (four pointers, no long load chain):
 // the select form costs them 36-84 B more of scratch spills.
-template <typename T>
+template <bool R = false, typename T>
 __device__ __forceinline__ T* gshift_br(T* p, size_t stride) {
     if (p == nullptr || stride == 0) return p;
     using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
-    return reinterpret_cast<T*>(reinterpret_cast<B*>(p) + size_t(blockIdx.y) * stride);
+    return reinterpret_cast<T*>(reinterpret_cast<B*>(p) + size_t(bg<R>()) * stride);
 }
 
 // Launch-error report (GLL_DEBUG=1 in the environment): which launcher failed and why.

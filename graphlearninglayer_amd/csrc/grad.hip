@@ -34,18 +34,19 @@ struct EdgeArgs {
     float* b;             // per-row b (auto)
     size_t wss;           // batched launches: workspace stride between graphs (bytes)
 
-    __device__ void to_graph() {   // move every workspace pointer to graph blockIdx.y
-        row_start = gshift(row_start, wss);
-        row_len = gshift(row_len, wss);
-        col = gshift(col, wss);
-        w = gshift(w, wss);
-        d2 = gshift(d2, wss);
-        eps = gshift(eps, wss);
-        P = gshift(P, wss);
-        Wadj = gshift(Wadj, wss);
-        knn_idx = gshift(knn_idx, wss);
-        S = gshift(S, wss);
-        b = gshift(b, wss);
+    template <bool R = false>
+    __device__ void to_graph() {   // move every workspace pointer to this block's graph
+        row_start = gshift<R>(row_start, wss);
+        row_len = gshift<R>(row_len, wss);
+        col = gshift<R>(col, wss);
+        w = gshift<R>(w, wss);
+        d2 = gshift<R>(d2, wss);
+        eps = gshift<R>(eps, wss);
+        P = gshift<R>(P, wss);
+        Wadj = gshift<R>(Wadj, wss);
+        knn_idx = gshift<R>(knn_idx, wss);
+        S = gshift<R>(S, wss);
+        b = gshift<R>(b, wss);
     }
 };
 
@@ -69,7 +70,7 @@ __global__ __launch_bounds__(256) void edge_coef_kernel(EdgeArgs a) {
     GLL_TRACE_SCOPE(0);
     a.to_graph();
     const int lane = lane_id();
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int i = bx() * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
     const int beg = a.row_start[i], end = beg + a.row_len[i];
     const float ei = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[i];
@@ -95,11 +96,11 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
                                                         float* __restrict__ out, size_t xs,
                                                         size_t gxs) {
     GLL_TRACE_SCOPE(1);
-    a.to_graph();
-    X = gshift(X, xs);
-    out = gshift(out, gxs);
+    a.to_graph<true>();
+    X = gshift<true>(X, xs);
+    out = gshift<true>(out, gxs);
     const int lane = lane_id();
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int i = bx<true>() * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
     const int d = a.d;
     const int beg = a.row_start[i], end = beg + a.row_len[i];
@@ -196,8 +197,9 @@ __global__ __launch_bounds__(256) void grad_chunk_kernel(EdgeArgs a, const float
     constexpr int EB = LPR >= 32 ? 8 : 16;   // neighbour rows in flight per lane
     const int lane = lane_id();
     const int gl = lane % LPR;                // lane inside the row's group
-    const int chunk = blockIdx.x % nch;
-    const int i = (blockIdx.x / nch) * (4 * RPW) + (threadIdx.x >> 6) * RPW + lane / LPR;
+    const int blk = bx();
+    const int chunk = blk % nch;
+    const int i = (blk / nch) * (4 * RPW) + (threadIdx.x >> 6) * RPW + lane / LPR;
     const bool live = i < a.n;
     const int ic = live ? i : 0;
     const int d = a.d;

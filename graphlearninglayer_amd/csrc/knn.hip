@@ -191,14 +191,14 @@ __global__ __launch_bounds__(1024) void gram_bf3_kernel(const float* __restrict_
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar row bases
     const int r = lane & 31, h = lane >> 5;
-    int bi = 0, rem = xcd_tile(blockIdx.x, gridDim.x);
+    int bi = 0, rem = xcd_tile(bx(), gridDim.x);
     while (rem >= T - bi) {
         rem -= T - bi;
         ++bi;
     }
     const int bj = bi + rem;
     {   // per-call reset of the counters the select kernel accumulates into
-        const int g = blockIdx.x * 1024 + tid;
+        const int g = bx() * 1024 + tid;
         if (g < GLL_ST_NWORDS) status[g] = 0;
         for (int q = g; q < n; q += gridDim.x * 1024) rev_cnt[q] = 0;
     }
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(1024) void gram_bf3s_kernel(const float* __restrict
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
-    const int b = xcd_tile(blockIdx.x, gridDim.x);
+    const int b = xcd_tile(bx(), gridDim.x);
     const bool dg = b < T;   // block-uniform
     int bi = b, bj = b, half = 0;
     if (!dg) {   // strictly-upper tile (b - T) / 2, row-major; half = feature phase = plane
@@ -326,7 +326,7 @@ __global__ __launch_bounds__(1024) void gram_bf3s_kernel(const float* __restrict
         bj = bi + 1 + rem;
     }
     {   // per-call reset of the counters the select kernel accumulates into
-        const int g = blockIdx.x * 1024 + tid;
+        const int g = bx() * 1024 + tid;
         if (g < GLL_ST_NWORDS) status[g] = 0;
         for (int q = g; q < n; q += gridDim.x * 1024) rev_cnt[q] = 0;
     }
@@ -432,14 +432,14 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
-    int bi = 0, rem = xcd_tile(blockIdx.x, gridDim.x);
+    int bi = 0, rem = xcd_tile(bx(), gridDim.x);
     while (rem >= T - bi) {
         rem -= T - bi;
         ++bi;
     }
     const int bj = bi + rem;
     {   // per-call reset of the counters the select kernel accumulates into
-        const int g = blockIdx.x * 1024 + tid;
+        const int g = bx() * 1024 + tid;
         if (g < GLL_ST_NWORDS) status[g] = 0;
         for (int q = g; q < n; q += gridDim.x * 1024) rev_cnt[q] = 0;
     }
@@ -581,9 +581,8 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
 // loads are in flight while stage k's 48 MFMAs per wave run.  Rows are 128 B in LDS with the
 // 16-B segments XOR-swizzled by (row >> 1) & 7 -- on the SOURCE address, the DMA writes
 // lane-linearly -- so the ds_read_b128 fragment reads of 16 consecutive rows hit 16 distinct
-// bank groups.  The stage wait is a counted vmcnt (this wave's 16 DMAs of the older stage) and
-// a raw s_barrier, so the prefetch stays in flight across it (cdna_hip_programming.md
-// "Pipelining across barriers").
+// bank groups.  One raw s_barrier per stage; the next stage's DMAs are issued between the
+// current stage's MFMA groups.
 // --------------------------------------------------------------------------------------
 constexpr int kPK = 64;                  // features per k-stage
 typedef __attribute__((address_space(3))) void lds_void;
@@ -603,12 +602,12 @@ __global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict
     status = gshift_br(status, wss);
     rev_cnt = gshift_br(rev_cnt, wss);
     {   // per-call reset of the counters the select kernel accumulates into
-        const int g = blockIdx.x * 256 + threadIdx.x;
+        const int g = bx() * 256 + threadIdx.x;
         if (g < GLL_ST_NWORDS) status[g] = 0;
         for (int q = g; q < n; q += gridDim.x * 256) rev_cnt[q] = 0;
     }
     const int lane = lane_id();
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int i = bx() * 4 + (threadIdx.x >> 6);
     if (i >= n) return;
     const float* xi = X + size_t(i) * d;
     float sq = 0.f;
@@ -630,26 +629,65 @@ __global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict
     if (lane == 0) nrm[i] = sq;
 }
 
+// Tile t of the upper triangle of T x T blocks in supertile order: supertiles of kSR x kSC
+// blocks, row-major, each walked row-major.  With the XCD-contiguous deal of xcd_tile, the ~32
+// tiles an XCD runs at once come from one or two supertiles, whose kSR + kSC row blocks
+// (512 KB each at d = 1024) mostly stay in that XCD's 4 MB L2, instead of a row-major run whose
+// 32 column blocks are streamed from the MALL once per tile.
+constexpr int kSR = 4, kSC = 8;
+__device__ __forceinline__ void supertile_tile(int t, int T, int& bi, int& bj) {
+    for (int I = 0; I * kSR < T; ++I) {
+        for (int J = (I * kSR) / kSC; J * kSC < T; ++J) {
+            int cnt = 0;
+#pragma unroll
+            for (int a = 0; a < kSR; ++a) {
+                const int r = I * kSR + a;
+                const int lo = max(r, J * kSC), hi = min(T, J * kSC + kSC);
+                cnt += r < T && hi > lo ? hi - lo : 0;
+            }
+            if (t < cnt) {
+                for (int a = 0; a < kSR; ++a) {
+                    const int r = I * kSR + a;
+                    const int lo = max(r, J * kSC), hi = min(T, J * kSC + kSC);
+                    const int c = r < T && hi > lo ? hi - lo : 0;
+                    if (t < c) {
+                        bi = r;
+                        bj = lo + t;
+                        return;
+                    }
+                    t -= c;
+                }
+            }
+            t -= cnt;
+        }
+    }
+    bi = bj = 0;   // not reached for t < T (T + 1) / 2
+}
+
+// One-dimensional grid over B graphs x T (T + 1) / 2 tiles: xcd_tile deals each XCD a
+// contiguous run of the graph-major sequence, so a batch's graphs are XCD-local too.
 __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__ Ph,
                                                       const __bf16* __restrict__ Pl,
                                                       const float* __restrict__ nrm, int n,
                                                       int dp, int T, float* __restrict__ D2,
                                                       int ld, size_t wss) {
-    Ph = gshift_br(Ph, wss);
-    Pl = gshift_br(Pl, wss);
-    nrm = gshift_br(nrm, wss);
-    D2 = gshift_br(D2, wss);
+    const int NT = T * (T + 1) / 2;
+    const int idx = xcd_tile(blockIdx.x, gridDim.x);
+    const int g = idx / NT;
+    {
+        const size_t off = size_t(g) * wss;   // graph g's workspace block
+        Ph = reinterpret_cast<const __bf16*>(reinterpret_cast<const char*>(Ph) + off);
+        Pl = reinterpret_cast<const __bf16*>(reinterpret_cast<const char*>(Pl) + off);
+        nrm = reinterpret_cast<const float*>(reinterpret_cast<const char*>(nrm) + off);
+        D2 = reinterpret_cast<float*>(reinterpret_cast<char*>(D2) + off);
+    }
     constexpr int kTP = 128 * kPK;                                  // bf16 per tile plane
     __shared__ __attribute__((aligned(16))) __bf16 sm[2 * 4 * kTP];  // 128 KiB: [buf][plane]
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
-    int bi = 0, rem = xcd_tile(blockIdx.x, gridDim.x);
-    while (rem >= T - bi) {
-        rem -= T - bi;
-        ++bi;
-    }
-    const int bj = bi + rem;
+    int bi, bj;
+    supertile_tile(idx - g * NT, T, bi, bj);
     const int wr = w >> 1, wc = w & 1;
     // this lane's DMA sources: 16 per stage = plane q >> 2, rows 8 c .. 8 c + 7 (c = (q & 3) 4 + w)
     // as 1 KiB pieces; lane -> row 8 c + lane / 8, LDS segment lane % 8 <- source segment
@@ -664,9 +702,10 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
         grow = grow < n ? grow : n - 1;
         src[q] = ((pl & 1) ? Pl : Ph) + size_t(grow) * dp + 8 * seg;
     }
-    auto issue = [&](int ks, int buf) {
+    // DMAs of stage ks into buffer buf, pieces [q0, q0 + 4)
+    auto issue4 = [&](int ks, int buf, int q0) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
+        for (int q = q0; q < q0 + 4; ++q) {
             const int pl = q >> 2, c = (q & 3) * 4 + w;
             __bf16* dst = sm + (buf * 4 + pl) * kTP + c * 8 * kPK;
             __builtin_amdgcn_global_load_lds(src[q] + ks * kPK, (lds_void*)dst, 16, 0, 0);
@@ -684,18 +723,21 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
         return *reinterpret_cast<const bf16x8*>(sm + (buf * 4 + pl) * kTP + row * kPK + 8 * pos);
     };
     const int nks = dp / kPK;
-    issue(0, 0);
+    // One wave per SIMD: the next stage's 16 DMAs are issued in four groups between this
+    // stage's MFMA groups, so their issue overlaps the MFMA pipe.  One barrier per stage: it
+    // orders stage ks's DMAs (each wave drained its own with vmcnt(0) first) before any
+    // fragment read, and every wave's reads of the buffer the next DMAs overwrite (stage ks-1's)
+    // before those DMAs are issued.
+#pragma unroll
+    for (int q0 = 0; q0 < 16; q0 += 4) issue4(0, 0, q0);
     for (int ks = 0; ks < nks; ++ks) {
         const int buf = ks & 1;
-        if (ks + 1 < nks) {
-            issue(ks + 1, buf ^ 1);
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // this wave's stage-ks DMAs
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();                          // every wave's stage-ks DMAs
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's stage-ks DMAs
+        __builtin_amdgcn_s_barrier();                          // every wave's
+        const bool more = ks + 1 < nks;
 #pragma unroll
         for (int kk = 0; kk < kPK / 16; ++kk) {
+            if (more) issue4(ks + 1, buf ^ 1, 4 * kk);
             bf16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
@@ -713,9 +755,8 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
                 }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();   // buffer `buf` is refilled by the next stage's DMAs
     }
+    __syncthreads();   // the last stage's reads are done before the diagonal epilogue reuses sm
     // epilogue: D2 = |a_i|^2 + |a_j|^2 - 2 <a_i, a_j>; C layout of 32x32: col = lane & 31,
     // row = (e & 3) + 8 (e >> 2) + 4 h
     float nj[2];
@@ -1203,7 +1244,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     __shared__ int s_cand[4][kWave];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
-    const int i = blockIdx.x * 4 + wv;
+    const int i = bx() * 4 + wv;
     if (i >= n) return;  // whole wave
 
     // 1-2) candidates: short per-lane lists + threshold merge, exact re-run when inexact.
@@ -1362,8 +1403,8 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
             launch_k(gram_split_kernel<true>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
         else
             launch_k(gram_split_kernel<false>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
-        launch_k(gram_pk_kernel, dim3(T * (T + 1) / 2, bt.B), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T,
-                 D2, L.ldD, bt.ws);
+        launch_k(gram_pk_kernel, dim3(unsigned(bt.B * T * (T + 1) / 2)), 256, 0, s, Ph, Pl, nrm,
+                 L.n, L.dp, T, D2, L.ldD, bt.ws);
         prof_end(GLL_K_GRAM, s);
         return launch_status("knn.hip:launch_gram(pk)");
     }

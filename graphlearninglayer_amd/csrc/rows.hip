@@ -316,7 +316,7 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
     __shared__ float ybuf[4][PRE ? kWave * kYPre : 1];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
-    const int i = blockIdx.x * 4 + wv;
+    const int i = bx() * 4 + wv;
     if (i >= a.n) return;
     const int Km1 = a.K - 1;
     int fi = -1;

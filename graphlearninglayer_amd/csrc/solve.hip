@@ -201,20 +201,20 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     const float* __restrict__ ell_w, size_t wss, size_t bs,
     size_t us, size_t sts) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    ell_col = gshift(ell_col, wss);
-    ell_w = gshift(ell_w, wss);
-    row_start = gshift_br(row_start, wss);   // batched launches: graph blockIdx.y
-    row_len = gshift_br(row_len, wss);
-    ucnt = gshift(ucnt, wss);
-    col = gshift_br(col, wss);
-    wv = gshift_br(wv, wss);
-    diag = gshift(diag, wss);
-    bsrc = gshift(bsrc, bs);
-    out64 = gshift_br(out64, us);
-    out32 = gshift_br(out32, wss);
-    st_nonconv = gshift_br(st_nonconv, sts);
-    st_iters = gshift_br(st_iters, sts);
-    const int c = blockIdx.x;
+    ell_col = gshift<true>(ell_col, wss);
+    ell_w = gshift<true>(ell_w, wss);
+    row_start = gshift_br<true>(row_start, wss);   // batched launches: graph blockIdx.y
+    row_len = gshift_br<true>(row_len, wss);
+    ucnt = gshift<true>(ucnt, wss);
+    col = gshift_br<true>(col, wss);
+    wv = gshift_br<true>(wv, wss);
+    diag = gshift<true>(diag, wss);
+    bsrc = gshift<true>(bsrc, bs);
+    out64 = gshift_br<true>(out64, us);
+    out32 = gshift_br<true>(out32, wss);
+    st_nonconv = gshift_br<true>(st_nonconv, sts);
+    st_iters = gshift_br<true>(st_iters, sts);
+    const int c = bx<true>();
     const int tid = threadIdx.x;
     float* red = smem;                                  // 96 floats of reduction scratch
     int* scan = reinterpret_cast<int*>(smem + 96);      // 16 ints of scan scratch
@@ -668,20 +668,20 @@ __global__ __launch_bounds__(NT) void cg_vr_kernel(
     float* __restrict__ out32, float rtol, int max_iter, int32_t* __restrict__ st_nonconv,
     int32_t* __restrict__ st_iters, size_t wss, size_t bs, size_t us, size_t sts) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    row_start = gshift(row_start, wss);
-    row_len = gshift(row_len, wss);
-    ucnt = gshift(ucnt, wss);
-    col = gshift(col, wss);
-    wv = gshift(wv, wss);
-    diag = gshift(diag, wss);
-    vrs = gshift(vrs, wss);
-    bsrc = gshift(bsrc, bs);
-    out64 = gshift_br(out64, us);
-    out32 = gshift_br(out32, wss);
-    st_nonconv = gshift_br(st_nonconv, sts);
-    st_iters = gshift_br(st_iters, sts);
+    row_start = gshift<true>(row_start, wss);
+    row_len = gshift<true>(row_len, wss);
+    ucnt = gshift<true>(ucnt, wss);
+    col = gshift<true>(col, wss);
+    wv = gshift<true>(wv, wss);
+    diag = gshift<true>(diag, wss);
+    vrs = gshift<true>(vrs, wss);
+    bsrc = gshift<true>(bsrc, bs);
+    out64 = gshift_br<true>(out64, us);
+    out32 = gshift_br<true>(out32, wss);
+    st_nonconv = gshift_br<true>(st_nonconv, sts);
+    st_iters = gshift_br<true>(st_iters, sts);
     constexpr int VCAP = NT * RV;
-    const int c = blockIdx.x;
+    const int c = bx<true>();
     const int tid = threadIdx.x;
     const int mp4 = (m + 3) & ~3;
     float* red = smem;                                   // 96 floats of reduction scratch
@@ -953,19 +953,19 @@ __global__ __launch_bounds__(NT) void cg_lds_kernel(
     float* __restrict__ gvec, int vec_in_lds, int32_t* __restrict__ st_nonconv,
     int32_t* __restrict__ st_iters, size_t wss, size_t bs, size_t us, size_t sts) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    row_start = gshift(row_start, wss);
-    row_len = gshift(row_len, wss);
-    ucnt = gshift(ucnt, wss);
-    col = gshift(col, wss);
-    wv = gshift(wv, wss);
-    diag = gshift(diag, wss);
-    bsrc = gshift(bsrc, bs);
-    out64 = gshift(out64, us);
-    out32 = gshift(out32, wss);
-    gvec = gshift(gvec, wss);
-    st_nonconv = gshift(st_nonconv, sts);
-    st_iters = gshift(st_iters, sts);
-    const int c = blockIdx.x;
+    row_start = gshift<true>(row_start, wss);
+    row_len = gshift<true>(row_len, wss);
+    ucnt = gshift<true>(ucnt, wss);
+    col = gshift<true>(col, wss);
+    wv = gshift<true>(wv, wss);
+    diag = gshift<true>(diag, wss);
+    bsrc = gshift<true>(bsrc, bs);
+    out64 = gshift<true>(out64, us);
+    out32 = gshift<true>(out32, wss);
+    gvec = gshift<true>(gvec, wss);
+    st_nonconv = gshift<true>(st_nonconv, sts);
+    st_iters = gshift<true>(st_iters, sts);
+    const int c = bx<true>();
     const int tid = threadIdx.x;
     float* red = smem;
     float* vb = vec_in_lds ? smem + 64 : gvec + size_t(c) * 5 * m;
@@ -1183,7 +1183,7 @@ __global__ __launch_bounds__(NT) void cg_csr_kernel(int m, int C, const int32_t*
                                                     int vec_in_lds, int32_t* __restrict__ iters,
                                                     int32_t* __restrict__ nonconv) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int c = blockIdx.x;
+    const int c = bx<true>();
     const int tid = threadIdx.x;
     float* red = smem;
     float* vb = vec_in_lds ? smem + 64 : gvec + size_t(c) * 5 * m;
