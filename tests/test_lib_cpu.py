@@ -52,8 +52,9 @@ def test_workspace_bytes_and_validation():
     lib = _lib.lib()
     p = G.make_problem(1000, 512, 500, 10, 10, 0.07, 1.0)
     nb = lib.gll_workspace_bytes(ct.byref(p))
-    # dominated by the n x n squared-distance matrix
-    assert 1000 * 1000 * 4 < nb < 1000 * 1000 * 4 + 8 * 2**20
+    # dominated by the n x n squared-distance planes (two at NS: the split-phase Gram) and the
+    # n x d hi/lo bf16 planes of the pre-split Gram (knn.hip gram_split_kernel)
+    assert 2 * 1000 * 1000 * 4 < nb < 2 * 1000 * 1000 * 4 + 1000 * 512 * 4 + 4 * 2**20
     bad = G.make_problem(1000, 512, 500, 10, 10, 0.07, 1.0)
     bad.K = 1
     assert lib.gll_workspace_bytes(ct.byref(bad)) == 0
