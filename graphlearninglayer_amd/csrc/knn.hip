@@ -932,7 +932,8 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // `tb` receives the D2 bits of the kc-th key (every column left out is >= it), or +inf when
 // fewer than kc valid columns exist (then every one of them is a candidate).
 template <int KC>
-__device__ __forceinline__ int merge_exact(uint64_t (&key)[KC], int kc, uint32_t& tb) {
+__device__ __forceinline__ int merge_exact(uint64_t (&key)[KC], int kc, uint32_t& tb,
+                                           uint32_t& gbits) {
     const int lane = lane_id();
     uint64_t mine = ~0ull;
     tb = 0x7F800000u;
@@ -942,6 +943,7 @@ __device__ __forceinline__ int merge_exact(uint64_t (&key)[KC], int kc, uint32_t
         if (best != ~0ull && t == kc - 1) tb = uint32_t(best >> 32);
         list_pop<KC>(key, best != ~0ull && key[0] == best);
     }
+    gbits = uint32_t(mine >> 32);
     return mine == ~0ull ? -1 : int(uint32_t(mine));
 }
 
@@ -977,8 +979,9 @@ __device__ __forceinline__ bool merge_fast(uint64_t (&key)[KS], int kc, int seen
 // candidates tie in; the caller then re-runs the exact merge.
 template <int KS>
 __device__ __forceinline__ bool merge_threshold(const uint64_t (&key)[KS], int kc, int seen,
-                                                int* __restrict__ cand, int& ci, int& kce,
-                                                uint32_t& tb) {
+                                                int* __restrict__ cand,
+                                                uint32_t* __restrict__ cgd, int& ci, int& kce,
+                                                uint32_t& tb, uint32_t& gbits) {
     const int lane = lane_id();
     uint32_t hv[KS];
 #pragma unroll
@@ -1018,12 +1021,16 @@ __device__ __forceinline__ bool merge_threshold(const uint64_t (&key)[KS], int k
     if (!redo) {   // a lane's entries <= T are a prefix of its sorted list
 #pragma unroll
         for (int s = 0; s < KS; ++s)
-            if (hv[s] <= T) cand[before + s] = int(uint32_t(key[s]));
+            if (hv[s] <= T) {
+                cand[before + s] = int(uint32_t(key[s]));
+                cgd[before + s] = hv[s];
+            }
     }
     __builtin_amdgcn_wave_barrier();   // a wave's LDS ops run in order: the reads see the stores
     asm volatile("" ::: "memory");
     kce = total;
     ci = (!redo && lane < total) ? cand[lane] : -1;
+    gbits = (!redo && lane < total) ? cgd[lane] : 0xFFFFFFFFu;
     return redo;
 }
 
@@ -1242,6 +1249,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     status = gshift(status, wss);
     status_pub = gshift(status_pub, sts);
     __shared__ int s_cand[4][kWave];
+    __shared__ uint32_t s_cgd[4][kWave];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
     const int i = bx() * 4 + wv;
@@ -1252,18 +1260,56 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     const float* row = D2 + size_t(i) * ld;
     constexpr int KS = KC <= 16 ? 4 : 8;
     int ci, kce;
-    uint32_t tb;
+    uint32_t tb, gb;   // gb: this lane's candidate's Gram D2 bits
     {
         uint64_t key[KS];
         const int seen = scan_row<KS, NP>(row, plane, n, ld, i, key);
         GLL_TRACE_PT(16);
-        const bool redo = merge_threshold<KS>(key, kc, seen, s_cand[wv], ci, kce, tb);
+        const bool redo = merge_threshold<KS>(key, kc, seen, s_cand[wv], s_cgd[wv], ci, kce, tb, gb);
         GLL_TRACE_PT(17);
         if (redo) {
             uint64_t full[KC];
             scan_row<KC, NP>(row, plane, n, ld, i, full);
-            ci = merge_exact<KC>(full, kc, tb);
+            ci = merge_exact<KC>(full, kc, tb, gb);
             kce = kc;
+        }
+    }
+    // 2b) drop the candidates the Gram's error bound already rules out, before their exact
+    //     distances are computed (each is a d-float row gather): with G = the (K-1)-th smallest
+    //     Gram D2 among the candidates and B its error bound (kGramErr, below), the exact
+    //     (K-1)-th distance is <= G + B, and a column whose exact d^2 is below that has Gram
+    //     D2 < G + 2B; candidates above G + 2B join the left-out columns (tb) that the
+    //     certificate of step 5 covers.  NS: 16 candidates -> ~9-10 re-ranked.
+    if (K >= 2 && kce > K - 1) {
+        const float g = ci >= 0 && lane < kce ? __uint_as_float(gb) : __builtin_inff();
+        int grk = 0;   // rank of (g, index) among the candidates
+        for (int u = 0; u < kce; ++u) {
+            const float gu = readlane_f(g, u);
+            const int cu = __builtin_amdgcn_readlane(ci, u);
+            grk += (gu < g || (gu == g && cu < ci)) ? 1 : 0;
+        }
+        const uint64_t kb = __ballot(lane < kce && ci >= 0 && grk == K - 2);
+        if (kb) {
+            const double G = double(readlane_f(g, int(__builtin_ctzll(kb))));
+            float a2 = row[0];
+#pragma unroll
+            for (int p = 1; p < NP; ++p) a2 += row[p * plane];
+            const double ai = sqrt(double(a2 > 0.f ? a2 : 0.f));
+            const double gp = G > 0.0 ? G : 0.0;
+            const double b0 = kGramErr * (2.0 * ai + sqrt(gp)) * (2.0 * ai + sqrt(gp));
+            const double r1 = 2.0 * ai + sqrt(gp + b0);
+            const double thr = G + 2.0 * kGramErr * r1 * r1;
+            const bool need = lane < kce && ci >= 0 && (grk < K - 1 || double(g) <= thr);
+            const bool drop = lane < kce && ci >= 0 && !need;
+            // the smallest dropped Gram D2 joins the left-out bound
+            const uint32_t dmin = wave_min_u32(drop ? gb : 0xFFFFFFFFu);
+            if (dmin < tb) tb = dmin;
+            const uint64_t nm = __ballot(need);
+            if (need) s_cand[wv][lanes_below(nm)] = ci;
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            kce = __popcll(nm);
+            ci = lane < kce ? s_cand[wv][lane] : -1;
         }
     }
     // 3) exact squared distances of the candidates, fp32.  PG passes per sweep for single
