@@ -1227,7 +1227,7 @@ __device__ __forceinline__ KnnPick knn_rescan(const float* __restrict__ row, siz
     return KnnPick{bd, bi};
 }
 
-template <int KC, bool VEC, int NP, int PG>
+template <int KC, bool VEC, int NP, int PG, int NU>
 __global__ __launch_bounds__(256) void knn_select_kernel(
     const float* __restrict__ D2, int ld, size_t plane, const float* __restrict__ X, int n, int d, int K,
     int kc, float eps_fixed, int auto_eps, int RCAP, int32_t* __restrict__ knn_idx,
@@ -1315,7 +1315,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     // 3) exact squared distances of the candidates, fp32.  PG passes per sweep for single
     //    graphs (one wave per SIMD anyway); batches keep PG = 1 (register pressure).
     const float* xi = X + size_t(i) * d;
-    double ce = double(exact_d2<VEC, PG, float>(X, xi, i, d, ci, 0, kce, __builtin_inff()));
+    double ce = double(exact_d2<VEC, PG, float, NU>(X, xi, i, d, ci, 0, kce, __builtin_inff()));
     GLL_TRACE_PT(18);
     if (ci < 0) ce = __builtin_inf();
     // 4) rank the candidates by (exact d^2, index); keep the K-1 nearest
@@ -1491,8 +1491,11 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     prof_begin(GLL_K_SELECT, s);
     const size_t plane = size_t(n) * L.ldD;
     const int planes = gram_planes(L, bt.B);
-#define GLL_SEL3(KCV, V, NPV)                                                                  \
-    launch_k((bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2> : knn_select_kernel<KCV, V, NPV, 1>), grid, 256, 0, s,  \
+// NU: 32-feature steps per exact-distance load batch -- d / 32 where d <= 128 (4), otherwise 16
+// (the loads of steps past d are clamped to row 0 and masked: 12 of 16 wasted at d = 128)
+#define GLL_SEL4(KCV, V, NPV, NUV)                                                             \
+    launch_k((bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2, NUV>                               \
+                        : knn_select_kernel<KCV, V, NPV, 1, NUV>), grid, 256, 0, s,            \
         L.at<float>(ws, L.D2), L.ldD, plane, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0,     \
         L.RCAP,                                                                                \
         L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \
@@ -1500,14 +1503,15 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
         L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub, bt.x, bt.ws, bt.st)
 #define GLL_SEL(KCV, V)                                                                        \
     do {                                                                                       \
-        if (planes == 2) GLL_SEL3(KCV, V, 2);                                                  \
-        else GLL_SEL3(KCV, V, 1);                                                              \
+        if (planes == 2) GLL_SEL4(KCV, V, 2, 16);                                              \
+        else if (L.d <= 128) GLL_SEL4(KCV, V, 1, 4);                                           \
+        else GLL_SEL4(KCV, V, 1, 16);                                                          \
     } while (0)
     if (KC == 16) { if (vec) GLL_SEL(16, true); else GLL_SEL(16, false); }
     else if (KC == 32) { if (vec) GLL_SEL(32, true); else GLL_SEL(32, false); }
     else { if (vec) GLL_SEL(64, true); else GLL_SEL(64, false); }
 #undef GLL_SEL
-#undef GLL_SEL3
+#undef GLL_SEL4
     prof_end(GLL_K_SELECT, s);
     return launch_status("knn.hip:launch_select");
 }
