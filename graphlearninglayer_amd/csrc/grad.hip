@@ -65,24 +65,93 @@ __device__ __forceinline__ float edge_gv(const EdgeArgs& a, int i, int j, float 
     return g * v;
 }
 
-// auto eps, pass 1: S_ij and b_i (also the fixed-eps S_ij of the feature-chunked gradient)
+// The same with row i's values of w and P already in registers and the class count a
+// compile-time bound CV >= C: all 2C loads of row j are issued before any is used (the loop
+// above is one dependent L2 round trip per class), and the sum runs in the same order, so the
+// two agree bitwise.
+template <int CV>
+struct RowWP {
+    float w[CV], p[CV];
+};
+template <int CV>
+__device__ __forceinline__ RowWP<CV> row_wp(const EdgeArgs& a, int i) {
+    RowWP<CV> r;
+    const float* wi = a.Wadj + size_t(i) * a.C;
+    const float* pi = a.P + size_t(i) * a.C;
+#pragma unroll
+    for (int c = 0; c < CV; ++c) {
+        const int cc = c < a.C ? c : 0;
+        r.w[c] = wi[cc];
+        r.p[c] = pi[cc];
+    }
+    return r;
+}
+template <int CV>
+__device__ __forceinline__ float edge_gv_r(const EdgeArgs& a, const RowWP<CV>& ri, int j,
+                                           float we, float ei) {
+    const float* wj = a.Wadj + size_t(j) * a.C;
+    const float* pj = a.P + size_t(j) * a.C;
+    float wv[CV], pv[CV];
+#pragma unroll
+    for (int c = 0; c < CV; ++c) {
+        const int cc = c < a.C ? c : 0;
+        wv[c] = wj[cc];
+        pv[c] = pj[cc];
+    }
+    float g = 0.f;
+#pragma unroll
+    for (int c = 0; c < CV; ++c)
+        if (c < a.C) g += (ri.w[c] - wv[c]) * (pv[c] - ri.p[c]);
+    const float ej = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[j];
+    const float v = -8.f * we / (ei * ej);   // GLL.py:217/234
+    return g * v;
+}
+
+// auto eps, pass 1: S_ij and b_i (also the fixed-eps S_ij of the feature-chunked gradient).
+// LPR lanes per row (rows are ~K..2K edges: a whole wave per row left most lanes idle), CV the
+// class bound of the register form (0: the generic loop).  Latency-bound -- three dependent
+// gathers per edge -- so the register budget (occupancy) is what the CV templating buys.
+template <int CV, int LPR>
 __global__ __launch_bounds__(256) void edge_coef_kernel(EdgeArgs a) {
     GLL_TRACE_SCOPE(0);
     a.to_graph();
+    constexpr int RPW = kWave / LPR;
     const int lane = lane_id();
-    const int i = bx() * 4 + (threadIdx.x >> 6);
-    if (i >= a.n) return;
-    const int beg = a.row_start[i], end = beg + a.row_len[i];
-    const float ei = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[i];
+    const int gl = lane % LPR;
+    const int i = bx() * (4 * RPW) + (threadIdx.x >> 6) * RPW + lane / LPR;
+    const bool live = i < a.n;
+    const int ic = live ? i : 0;
+    const int beg = live ? a.row_start[ic] : 0;
+    const int end = live ? beg + a.row_len[ic] : 0;
+    const float ei = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[ic];
     float bpart = 0.f;
-    for (int e = beg + lane; e < end; e += kWave) {
-        float g;
-        const float s = edge_gv(a, i, a.col[e], a.w[e], ei, g);
-        a.S[e] = s;
-        bpart += s * a.d2[e];   // G d^2 V
+    if constexpr (CV > 0) {
+        const RowWP<CV> ri = row_wp<CV>(a, ic);
+        for (int e = beg + gl; e < end; e += LPR) {
+            const float s = edge_gv_r<CV>(a, ri, a.col[e], a.w[e], ei);
+            a.S[e] = s;
+            bpart += s * a.d2[e];   // G d^2 V
+        }
+    } else {
+        for (int e = beg + gl; e < end; e += LPR) {
+            float g;
+            const float s = edge_gv(a, ic, a.col[e], a.w[e], ei, g);
+            a.S[e] = s;
+            bpart += s * a.d2[e];   // G d^2 V
+        }
     }
-    bpart = wave_sum(bpart);
-    if (lane == 0) a.b[i] = bpart / (2.f * ei * ei);  // modV = d^2 V / (2 eps_i^2), GLL.py:218
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) bpart += __shfl_xor(bpart, o, LPR);
+    if (live && gl == 0) a.b[i] = bpart / (2.f * ei * ei);  // modV = d^2 V / (2 eps_i^2), GLL.py:218
+}
+
+template <int CV>
+static void launch_edge_coef(const EdgeArgs& a, const Batch& bt, int lpr, hipStream_t s) {
+    const unsigned rows = 4u * unsigned(kWave / lpr);
+    const dim3 grid((unsigned(a.n) + rows - 1) / rows, bt.B);
+    if (lpr == 16) launch_k(edge_coef_kernel<CV, 16>, grid, 256, 0, s, a);
+    else if (lpr == 32) launch_k(edge_coef_kernel<CV, 32>, grid, 256, 0, s, a);
+    else launch_k(edge_coef_kernel<CV, 64>, grid, 256, 0, s, a);
 }
 
 // out_i = sum_e coef_e (x_i - x_{col_e}) in the difference form: translation-invariant like the
@@ -182,9 +251,9 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
 // column reach the group's lanes by a width-LPR shuffle.  The per-edge coefficient is recomputed
 // per chunk (C-wide gathers from the n x C arrays, L2-resident).  Same edge order and summation
 // per element as grad_spmm_kernel, so the two agree bitwise.
-// COEF: 0 = fixed eps, coefficient G V per edge inline; 1 = auto eps (S and b from
-// edge_coef_kernel); 2 = fixed eps, S from edge_coef_kernel (the inline form would be recomputed
-// by every chunk: 4 C gathers per edge, which at NCH = 8 cost more than the chunking saves).
+// COEF: 1 = auto eps (S and b from edge_coef_kernel); 2 = fixed eps, S from edge_coef_kernel
+// (an inline G V would be recomputed by every chunk: 2C + 1 gathers per edge, which at NCH = 8
+// cost more than the chunking saves).
 template <int COEF, int LPR>
 __global__ __launch_bounds__(256) void grad_chunk_kernel(EdgeArgs a, const float* __restrict__ X,
                                                          float* __restrict__ out, int nch,
@@ -227,11 +296,8 @@ __global__ __launch_bounds__(256) void grad_chunk_kernel(EdgeArgs a, const float
                 cf = a.S[e];
                 if (cj == kth_i) cf -= b_i;
                 if (a.knn_idx[size_t(cj) * a.K + a.K - 1] == i) cf -= a.b[cj];
-            } else if constexpr (COEF == 2) {
-                cf = a.S[e];
             } else {
-                float g;
-                cf = edge_gv(a, ic, cj, a.w[e], ei, g);
+                cf = a.S[e];
             }
         }
         const int cnt = min(LPR, end - e0);
@@ -254,13 +320,16 @@ __global__ __launch_bounds__(256) void grad_chunk_kernel(EdgeArgs a, const float
         __builtin_nontemporal_store(acc, reinterpret_cast<f32x4*>(out + size_t(i) * d + k));
 }
 
-// Whether the feature-chunked gradient runs: 16-B rows with d >= 128, and a graph whose X does
-// not fit an XCD's 4 MB L2 (measured, tools/ab_flags.py --flags 2048,4096: stress grad 192 ->
-// 94 us; NS 8.7 -> 13.7 us and B = 64 NS 197 -> 527 us, where X already fits and the chunks
-// only multiply the per-edge work), or forced by the flags.
-static bool grad_use_chunks(const Layout& L, bool vec) {
+// Whether the feature-chunked gradient runs: 16-B rows with d >= 128, and either a graph whose X
+// does not fit an XCD's 4 MB L2 or a batch of narrow graphs (d < 256, where a wave per row
+// leaves lanes idle), or forced by the flags.  Measured (tools/ab_flags.py --flags 0,2048,
+// edge coefficients + gradient): stress 31 + 95 vs 194 us; FullySup B = 64 165 + 103 vs 307 us;
+// NS B = 64 55 + 147 vs 183 us and NS/FullySup single graphs a tie (X already fits; the
+// chunks only add the coefficient pass).
+static bool grad_use_chunks(const Layout& L, const Batch& bt, bool vec) {
     if (!vec || L.d < 128 || (L.d & 3) || (L.flags & GLL_FLAG_GRAD_ROWS)) return false;
-    return (L.flags & GLL_FLAG_GRAD_CHUNK) || size_t(L.n) * L.d * 4 > (size_t(4) << 20);
+    return (L.flags & GLL_FLAG_GRAD_CHUNK) || (bt.B > 1 && L.d < 256) ||
+           size_t(L.n) * L.d * 4 > (size_t(4) << 20);
 }
 
 // LPR = the power of two nearest d / 32 in [16, 64], NCH = ceil(d / (4 LPR)) chunks.
@@ -325,10 +394,15 @@ hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, cons
     a.b = L.at<float>(ws, L.b);
     a.wss = bt.ws;
     hipError_t e;
-    const bool chunk = grad_use_chunks(L, vec);
+    const bool chunk = grad_use_chunks(L, bt, vec);
     if (auto_eps || chunk) {   // per-edge S (and b) first
+        const int lpr = L.K <= 40 ? 16 : 32;   // tools/ab_flags.py: 16 lanes per row beat 32/64
         prof_begin(GLL_K_EDGE, s);
-        launch_k(edge_coef_kernel, dim3((L.n + 3) / 4, bt.B), 256, 0, s, a);
+        if (L.C <= 2) launch_edge_coef<2>(a, bt, lpr, s);
+        else if (L.C <= 4) launch_edge_coef<4>(a, bt, lpr, s);
+        else if (L.C <= 8) launch_edge_coef<8>(a, bt, lpr, s);
+        else if (L.C <= 16) launch_edge_coef<16>(a, bt, lpr, s);
+        else launch_edge_coef<0>(a, bt, lpr, s);
         prof_end(GLL_K_EDGE, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
