@@ -31,6 +31,7 @@ FLAG_GRAM_INLINE = 8192  # gll_problem.flags: 128-tile Gram with the inline spli
 ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
 ST_KNN_RESCAN = 5   # kNN rows re-ranked over every column under the Gram error bound
 ST_SOLVE_FAILED = 6   # a whole-GPU CG lost a grid barrier: outputs NaN, raised as an error
+ST_KNN_MERGE = 7   # kNN rows that took the exact candidate merge (diagnostic)
 ST_NWORDS = 16
 K_GRAM, K_SELECT, K_FINALIZE, K_CG, K_EDGE, K_GRAD = range(6)
 K_COUNT = 6

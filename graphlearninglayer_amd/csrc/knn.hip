@@ -1068,9 +1068,10 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // ranks in float64 -- used where fp32 cannot separate two candidates.  Either
 // way the (i, j) and (j, i) sums run the same lane mapping on negated differences: bitwise
 // symmetric for the same ACC.  Lanes outside [lo, hi) keep `ce`.
-template <bool VEC, int PG, typename ACC, int NU = 16>
+template <bool VEC, int PG, typename ACC, int NU = 16, bool XL = false>
 __device__ __forceinline__ ACC exact_d2(const float* __restrict__ X, const float* __restrict__ xi,
-                                        int i, int d, int ci, int lo, int hi, ACC ce) {
+                                        int i, int d, int ci, int lo, int hi, ACC ce,
+                                        const float* xs = nullptr) {
     constexpr bool F64 = std::is_same<ACC, double>::value;
     const int lane = lane_id();
     const int grp = lane >> 3, sub = lane & 7;
@@ -1091,15 +1092,18 @@ __device__ __forceinline__ ACC exact_d2(const float* __restrict__ X, const float
 #pragma unroll
             for (int u = 0; u < NU; ++u) {   // straight-line: every load issued before use
                 const int k = kb + 32 * u + 4 * sub;
-                va[u] = load4_raw<VEC>(xi, k, d);
+                if constexpr (!XL) va[u] = load4_raw<VEC>(xi, k, d);
 #pragma unroll
                 for (int g2 = 0; g2 < PG; ++g2) vb[g2][u] = load4_raw<VEC>(xj[g2], k, d);
+
             }
 #pragma unroll
             for (int g2 = 0; g2 < PG; ++g2) {
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {   // same order from either end: symmetric
                     const int k = kb + 32 * u + 4 * sub;
+                    if constexpr (XL)   // x_i from the wave's LDS copy, read at use
+                        va[u] = *reinterpret_cast<const f32x4*>(xs + k);
                     if constexpr (F64) {
                         const f32x4 a = mask4<VEC>(va[u], k, d), b = mask4<VEC>(vb[g2][u], k, d);
                         const double d0 = double(a.x) - double(b.x), d1 = double(a.y) - double(b.y);
@@ -1227,8 +1231,10 @@ __device__ __forceinline__ KnnPick knn_rescan(const float* __restrict__ row, siz
     return KnnPick{bd, bi};
 }
 
-template <int KC, bool VEC, int NP, int PG, int NU>
-__global__ __launch_bounds__(256) void knn_select_kernel(
+// XQ > 0: x_i staged in LDS, d <= 256 XQ
+template <int KC, bool VEC, int NP, int PG, int NU, int XQ = 0, bool R = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XQ > 0 && NU <= 8 ? 6 : 1)))
+void knn_select_kernel(
     const float* __restrict__ D2, int ld, size_t plane, const float* __restrict__ X, int n, int d, int K,
     int kc, float eps_fixed, int auto_eps, int RCAP, int32_t* __restrict__ knn_idx,
     float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ rev_cnt,
@@ -1237,23 +1243,37 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     size_t sts) {
     GLL_TRACE_SCOPE(1);
     GLL_TRACE_PT(20);
-    D2 = gshift(D2, wss);
-    X = gshift(X, xs);
-    knn_idx = gshift(knn_idx, wss);
-    knn_d2 = gshift(knn_d2, wss);
-    eps = gshift(eps, wss);
-    rev_cnt = gshift(rev_cnt, wss);
-    rev_idx = gshift(rev_idx, wss);
-    rev_d2 = gshift(rev_d2, wss);
-    ovf = gshift(ovf, wss);
-    status = gshift(status, wss);
-    status_pub = gshift(status_pub, sts);
+    D2 = gshift<R>(D2, wss);
+    X = gshift<R>(X, xs);
+    knn_idx = gshift<R>(knn_idx, wss);
+    knn_d2 = gshift<R>(knn_d2, wss);
+    eps = gshift<R>(eps, wss);
+    rev_cnt = gshift<R>(rev_cnt, wss);
+    rev_idx = gshift<R>(rev_idx, wss);
+    rev_d2 = gshift<R>(rev_d2, wss);
+    ovf = gshift<R>(ovf, wss);
+    status = gshift<R>(status, wss);
+    status_pub = gshift<R>(status_pub, sts);
     __shared__ int s_cand[4][kWave];
     __shared__ uint32_t s_cgd[4][kWave];
+    constexpr bool XL = XQ > 0;
+    __shared__ float s_xi[XL ? 4 : 1][XL ? 256 * XQ : 1];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
-    const int i = bx() * 4 + wv;
+    const int i = bx<R>() * 4 + wv;
     if (i >= n) return;  // whole wave
+    // XL: x_i is staged once in LDS (its loads ride under the D2 scan's), so the exact
+    // distances hold only the candidates' rows in registers (occupancy) and do not re-load x_i
+    // per sweep.  Features past d are zero (masked at use anyway).
+    f32x4 xr[XL ? XQ : 1];
+    if constexpr (XL) {
+        const float* xg = X + size_t(i) * d;
+#pragma unroll
+        for (int q = 0; q < XQ; ++q) {
+            const int k = 4 * lane + 256 * q;
+            xr[q] = k < d ? *reinterpret_cast<const f32x4*>(xg + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
 
     // 1-2) candidates: short per-lane lists + threshold merge, exact re-run when inexact.
     //      tb: D2 bits every non-candidate column is >= to (+inf: all valid columns taken)
@@ -1265,9 +1285,15 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
         uint64_t key[KS];
         const int seen = scan_row<KS, NP>(row, plane, n, ld, i, key);
         GLL_TRACE_PT(16);
+        if constexpr (XL) {
+#pragma unroll
+            for (int q = 0; q < XQ; ++q)
+                *reinterpret_cast<f32x4*>(&s_xi[wv][4 * lane + 256 * q]) = xr[q];
+        }
         const bool redo = merge_threshold<KS>(key, kc, seen, s_cand[wv], s_cgd[wv], ci, kce, tb, gb);
         GLL_TRACE_PT(17);
         if (redo) {
+            if (lane == 0) atomicAdd(&status_pub[GLL_ST_KNN_MERGE], 1);
             uint64_t full[KC];
             scan_row<KC, NP>(row, plane, n, ld, i, full);
             ci = merge_exact<KC>(full, kc, tb, gb);
@@ -1315,7 +1341,10 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     // 3) exact squared distances of the candidates, fp32.  PG passes per sweep for single
     //    graphs (one wave per SIMD anyway); batches keep PG = 1 (register pressure).
     const float* xi = X + size_t(i) * d;
-    double ce = double(exact_d2<VEC, PG, float, NU>(X, xi, i, d, ci, 0, kce, __builtin_inff()));
+    __builtin_amdgcn_wave_barrier();   // the LDS copy of x_i (written above) is complete
+    asm volatile("" ::: "memory");
+    double ce = double(exact_d2<VEC, PG, float, NU, XL>(X, xi, i, d, ci, 0, kce,
+                                                        __builtin_inff(), &s_xi[wv][0]));
     GLL_TRACE_PT(18);
     if (ci < 0) ce = __builtin_inf();
     // 4) rank the candidates by (exact d^2, index); keep the K-1 nearest
@@ -1491,11 +1520,14 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     prof_begin(GLL_K_SELECT, s);
     const size_t plane = size_t(n) * L.ldD;
     const int planes = gram_planes(L, bt.B);
-// NU: 32-feature steps per exact-distance load batch -- d / 32 where d <= 128 (4), otherwise 16
-// (the loads of steps past d are clamped to row 0 and masked: 12 of 16 wasted at d = 128)
-#define GLL_SEL4(KCV, V, NPV, NUV)                                                             \
-    launch_k((bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2, NUV>                               \
-                        : knn_select_kernel<KCV, V, NPV, 1, NUV>), grid, 256, 0, s,            \
+// Batched launches (PG = 1) stage x_i in LDS (XQ quarters of 256 features, d <= 1024) and run at
+// 6 waves per SIMD: measured at B = 64 NS, select 259 -> 214 us (XQ = 2, NU = 8; the NU = 16
+// batch of loads held 120 VGPRs, 4 waves).  NU: 32-feature steps per exact-distance load batch,
+// d / 32 up to 8 for batches (16 for single graphs, whose one wave per SIMD has registers to
+// spare); the loads of steps past d are clamped to row 0 and masked.
+#define GLL_SEL4(KCV, V, NPV, NUS, NUB, XQV)                                                   \
+    launch_k((bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2, NUS>                               \
+                        : knn_select_kernel<KCV, V, NPV, 1, NUB, (V ? XQV : 0)>), grid, 256, 0, s, \
         L.at<float>(ws, L.D2), L.ldD, plane, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0,     \
         L.RCAP,                                                                                \
         L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \
@@ -1503,9 +1535,12 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
         L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub, bt.x, bt.ws, bt.st)
 #define GLL_SEL(KCV, V)                                                                        \
     do {                                                                                       \
-        if (planes == 2) GLL_SEL4(KCV, V, 2, 16);                                              \
-        else if (L.d <= 128) GLL_SEL4(KCV, V, 1, 4);                                           \
-        else GLL_SEL4(KCV, V, 1, 16);                                                          \
+        if (planes == 2) GLL_SEL4(KCV, V, 2, 16, 16, 0);                                       \
+        else if (L.d <= 128) GLL_SEL4(KCV, V, 1, 4, 4, 1);                                     \
+        else if (L.d <= 256) GLL_SEL4(KCV, V, 1, 16, 8, 1);                                    \
+        else if (L.d <= 512) GLL_SEL4(KCV, V, 1, 16, 8, 2);                                    \
+        else if (L.d <= 1024) GLL_SEL4(KCV, V, 1, 16, 8, 4);                                   \
+        else GLL_SEL4(KCV, V, 1, 16, 16, 0);                                                   \
     } while (0)
     if (KC == 16) { if (vec) GLL_SEL(16, true); else GLL_SEL(16, false); }
     else if (KC == 32) { if (vec) GLL_SEL(32, true); else GLL_SEL(32, false); }

@@ -45,6 +45,8 @@ extern "C" {
 #define GLL_ST_SOLVE_FAILED 6  /* nonzero: a whole-GPU CG lost a grid barrier (a workgroup never
                                 * arrived); that solve's outputs were written as NaN.  The
                                 * Python layer raises RuntimeError on it */
+#define GLL_ST_KNN_MERGE 7     /* kNN rows whose short candidate lists may have dropped a column:
+                                * the exact merge ran instead (diagnostic count) */
 #define GLL_ST_NWORDS 16
 
 /* gll_problem.flags */

@@ -210,7 +210,10 @@ def test_duplicate_points_and_ties():
     Y = np.eye(10, dtype=np.float32)[lab[:base]]
     gb = rng.standard_normal((n - base, 10))
     U, grad = _run(X, Y, 0.07, 1.0, k, gb)
-    ind = _gpu_knn(X, k, 1.0)["knn_idx"].cpu().numpy()
+    from graphlearninglayer_amd import _lib
+    g = _gpu_knn(X, k, 1.0)
+    ind = g["knn_idx"].cpu().numpy()
+    assert int(g["status"][_lib.ST_KNN_MERGE].item()) > 0   # > 64 ties: the exact merge ran
     assert O.knn_set_mismatch(X, ind, k) == []
     Uo, st = O.forward(X, Y, 0.07, 1.0, k, knn=(ind, None))
     assert O.rel_err(U, Uo) < TOL
@@ -359,6 +362,28 @@ def test_batched_graphs_equal_single_calls_bitwise(cfg, eps, ydt, exact):
         else:
             assert O.rel_err(Ub[g].detach().cpu().numpy(), U1) <= 1e-5
             assert O.rel_err(Xb.grad[g].cpu().numpy(), gx1) <= 1e-5
+
+
+def test_batched_duplicates_match_single_calls():
+    """Batched selection (x_i staged in LDS, 6 waves per SIMD) on graphs with > 64 tied
+    candidates, where the exact merge runs: each graph's kNN, U and grad_X agree with its
+    single call (whose selection keeps x_i in registers)."""
+    GLL = _gll()
+    rng = np.random.default_rng(8)
+    n, d, base, k, B = 600, 40, 100, 10, 2
+    Xs = rng.standard_normal((B, n, d)).astype(np.float32)
+    Xs /= np.linalg.norm(Xs, axis=2, keepdims=True)
+    Xs[:, 400:480] = Xs[:, 399:400]
+    Xs[1, 200:230] = Xs[1, 199]
+    Y = np.eye(10, dtype=np.float32)[np.arange(base) % 10]
+    G = rng.standard_normal((B, n - base, 10))
+    Xb = torch.from_numpy(Xs).cuda().requires_grad_(True)
+    Ub = GLL.LaplaceLearningSparseHard.apply(Xb, torch.from_numpy(Y).cuda(), 0.07, 1.0, k)
+    Ub.backward(torch.from_numpy(G).cuda())
+    for g in range(B):
+        U1, gx1 = _run(Xs[g], Y, 0.07, 1.0, k, G[g])
+        assert O.rel_err(Ub[g].detach().cpu().numpy(), U1) <= 1e-5
+        assert O.rel_err(Xb.grad[g].cpu().numpy(), gx1) <= 1e-5
 
 
 def test_batched_shared_labels_python_and_cpp_paths_agree():
