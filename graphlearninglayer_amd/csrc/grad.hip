@@ -58,7 +58,7 @@ __device__ __forceinline__ float edge_gv(const EdgeArgs& a, int i, int j, float 
     const float* pi = a.P + size_t(i) * a.C;
     const float* pj = a.P + size_t(j) * a.C;
     float g = 0.f;
-    for (int c = 0; c < a.C; ++c) g += (wi[c] - wj[c]) * (pj[c] - pi[c]);
+    for (int c = 0; c < a.C; ++c) g = __builtin_fmaf(wi[c] - wj[c], pj[c] - pi[c], g);
     gout = g;
     const float ej = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[j];
     const float v = -8.f * we / (ei * ej);   // GLL.py:217/234
@@ -67,41 +67,53 @@ __device__ __forceinline__ float edge_gv(const EdgeArgs& a, int i, int j, float 
 
 // The same with row i's values of w and P already in registers and the class count a
 // compile-time bound CV >= C: all 2C loads of row j are issued before any is used (the loop
-// above is one dependent L2 round trip per class), and the sum runs in the same order, so the
-// two agree bitwise.
+// above is one dependent L2 round trip per class), and the sum runs in the same order with
+// explicit fmas (the unrolled form is otherwise vectorised into packed multiplies and adds,
+// which round twice), so the two agree bitwise.
 template <int CV>
 struct RowWP {
     float w[CV], p[CV];
 };
+// CV < 0: exactly -CV classes (even), rows loaded as 8-B pairs (the n x C rows are 8-B aligned
+// when C is even) -- C / 2 loads per array instead of CV.
 template <int CV>
-__device__ __forceinline__ RowWP<CV> row_wp(const EdgeArgs& a, int i) {
-    RowWP<CV> r;
+__device__ __forceinline__ void load_wp(const EdgeArgs& a, int i, float* w, float* p) {
+    constexpr int N = CV < 0 ? -CV : CV;
     const float* wi = a.Wadj + size_t(i) * a.C;
     const float* pi = a.P + size_t(i) * a.C;
+    if constexpr (CV < 0) {
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int c = 0; c < CV; ++c) {
-        const int cc = c < a.C ? c : 0;
-        r.w[c] = wi[cc];
-        r.p[c] = pi[cc];
+        for (int c = 0; c < N; c += 2) {
+            const f32x2 u = *reinterpret_cast<const f32x2*>(wi + c);
+            const f32x2 v = *reinterpret_cast<const f32x2*>(pi + c);
+            w[c] = u.x, w[c + 1] = u.y, p[c] = v.x, p[c + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            const int cc = c < a.C ? c : 0;
+            w[c] = wi[cc];
+            p[c] = pi[cc];
+        }
     }
+}
+template <int CV>
+__device__ __forceinline__ RowWP<CV < 0 ? -CV : CV> row_wp(const EdgeArgs& a, int i) {
+    RowWP<CV < 0 ? -CV : CV> r;
+    load_wp<CV>(a, i, r.w, r.p);
     return r;
 }
 template <int CV>
-__device__ __forceinline__ float edge_gv_r(const EdgeArgs& a, const RowWP<CV>& ri, int j,
-                                           float we, float ei) {
-    const float* wj = a.Wadj + size_t(j) * a.C;
-    const float* pj = a.P + size_t(j) * a.C;
-    float wv[CV], pv[CV];
-#pragma unroll
-    for (int c = 0; c < CV; ++c) {
-        const int cc = c < a.C ? c : 0;
-        wv[c] = wj[cc];
-        pv[c] = pj[cc];
-    }
+__device__ __forceinline__ float edge_gv_r(const EdgeArgs& a, const RowWP<CV < 0 ? -CV : CV>& ri,
+                                           int j, float we, float ei) {
+    constexpr int N = CV < 0 ? -CV : CV;
+    float wv[N], pv[N];
+    load_wp<CV>(a, j, wv, pv);
     float g = 0.f;
 #pragma unroll
-    for (int c = 0; c < CV; ++c)
-        if (c < a.C) g += (ri.w[c] - wv[c]) * (pv[c] - ri.p[c]);
+    for (int c = 0; c < N; ++c)
+        if (CV < 0 || c < a.C) g = __builtin_fmaf(ri.w[c] - wv[c], pv[c] - ri.p[c], g);
     const float ej = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[j];
     const float v = -8.f * we / (ei * ej);   // GLL.py:217/234
     return g * v;
@@ -125,8 +137,8 @@ __global__ __launch_bounds__(256) void edge_coef_kernel(EdgeArgs a) {
     const int end = live ? beg + a.row_len[ic] : 0;
     const float ei = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[ic];
     float bpart = 0.f;
-    if constexpr (CV > 0) {
-        const RowWP<CV> ri = row_wp<CV>(a, ic);
+    if constexpr (CV != 0) {
+        const auto ri = row_wp<CV>(a, ic);
         for (int e = beg + gl; e < end; e += LPR) {
             const float s = edge_gv_r<CV>(a, ri, a.col[e], a.w[e], ei);
             a.S[e] = s;
@@ -206,8 +218,10 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
         // lanes own feature columns: accumulate coef_e * x_j in edge order, EB rows of X in
         // flight per batch (padded slots carry coefficient 0 on row i itself)
         const int cnt = min(kWave, end - e0);
+        // batches (not WIDE) at ND = 2 take 4 rows per batch: 70 instead of 110 VGPRs, 7 waves
+        // per SIMD instead of 4 (B = 64 NS 182 -> 170 us)
         constexpr int EB0 = ND <= 2 ? 8 : (ND <= 4 ? 4 : (ND <= 8 ? 2 : 1));
-        constexpr int EB = WIDE ? 2 * EB0 : EB0;
+        constexpr int EB = WIDE ? 2 * EB0 : (ND == 2 ? 4 : EB0);
         for (int t0 = 0; t0 < cnt; t0 += EB) {
             float s[EB];
             f32x4 v[EB][ND];
@@ -323,8 +337,8 @@ __global__ __launch_bounds__(256) void grad_chunk_kernel(EdgeArgs a, const float
 // Whether the feature-chunked gradient runs: 16-B rows with d >= 128, and either a graph whose X
 // does not fit an XCD's 4 MB L2 or a batch of narrow graphs (d < 256, where a wave per row
 // leaves lanes idle), or forced by the flags.  Measured (tools/ab_flags.py --flags 0,2048,
-// edge coefficients + gradient): stress 31 + 95 vs 194 us; FullySup B = 64 165 + 103 vs 307 us;
-// NS B = 64 55 + 147 vs 183 us and NS/FullySup single graphs a tie (X already fits; the
+// edge coefficients + gradient): stress 16 + 94 vs 194 us; FullySup B = 64 61 + 102 vs 309 us;
+// NS B = 64 26 + 146 vs 170 us and NS/FullySup single graphs a tie (X already fits; the
 // chunks only add the coefficient pass).
 static bool grad_use_chunks(const Layout& L, const Batch& bt, bool vec) {
     if (!vec || L.d < 128 || (L.d & 3) || (L.flags & GLL_FLAG_GRAD_ROWS)) return false;
@@ -398,11 +412,21 @@ hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, cons
     if (auto_eps || chunk) {   // per-edge S (and b) first
         const int lpr = L.K <= 40 ? 16 : 32;   // tools/ab_flags.py: 16 lanes per row beat 32/64
         prof_begin(GLL_K_EDGE, s);
-        if (L.C <= 2) launch_edge_coef<2>(a, bt, lpr, s);
-        else if (L.C <= 4) launch_edge_coef<4>(a, bt, lpr, s);
-        else if (L.C <= 8) launch_edge_coef<8>(a, bt, lpr, s);
-        else if (L.C <= 16) launch_edge_coef<16>(a, bt, lpr, s);
-        else launch_edge_coef<0>(a, bt, lpr, s);
+        switch (L.C) {   // even C <= 16: exact count, paired loads; else a bound, or the loop
+            case 2: launch_edge_coef<-2>(a, bt, lpr, s); break;
+            case 4: launch_edge_coef<-4>(a, bt, lpr, s); break;
+            case 6: launch_edge_coef<-6>(a, bt, lpr, s); break;
+            case 8: launch_edge_coef<-8>(a, bt, lpr, s); break;
+            case 10: launch_edge_coef<-10>(a, bt, lpr, s); break;
+            case 12: launch_edge_coef<-12>(a, bt, lpr, s); break;
+            case 14: launch_edge_coef<-14>(a, bt, lpr, s); break;
+            case 16: launch_edge_coef<-16>(a, bt, lpr, s); break;
+            default:
+                if (L.C <= 4) launch_edge_coef<4>(a, bt, lpr, s);
+                else if (L.C <= 8) launch_edge_coef<8>(a, bt, lpr, s);
+                else if (L.C <= 16) launch_edge_coef<16>(a, bt, lpr, s);
+                else launch_edge_coef<0>(a, bt, lpr, s);
+        }
         prof_end(GLL_K_EDGE, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
