@@ -1465,7 +1465,9 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
     // 128-tiles when there are enough of them to fill the chip twice (large graphs and batches;
     // a single NS graph has only 36); 64-tiles otherwise
     const int T = (L.n + 127) / 128;
-    if (!(L.flags & GLL_FLAG_GRAM_NARROW) && int64_t(bt.B) * T * (T + 1) / 2 >= 512 &&
+    // pre-split GEMM from 256 tiles (NS B = 8, 288 tiles: 58 -> 45 us; a single FullySup graph,
+    // 78 tiles, stays on the 64-tile kernel: 17.5 against 21.6 us)
+    if (!(L.flags & GLL_FLAG_GRAM_NARROW) && int64_t(bt.B) * T * (T + 1) / 2 >= 256 &&
         !(L.flags & GLL_FLAG_GRAM_INLINE)) {
         // split once (one pass over X), then the LDS-DMA bf16 GEMM over 128-tiles
         __bf16* Ph = L.at<__bf16>(ws, L.xhi);
