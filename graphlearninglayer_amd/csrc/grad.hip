@@ -172,7 +172,11 @@ static void launch_edge_coef(const EdgeArgs& a, const Batch& bt, int lpr, hipStr
 // differences of nearby rows are exact).  AUTO selects the coefficient form
 // WIDE (single-graph launches, where occupancy is not the limit): twice the x_j rows in
 // flight per batch -- an NS row's ~13 neighbours in one memory round trip instead of two.
-template <bool AUTO, int ND, bool VEC, bool WIDE>
+// CV (fixed eps): the class bound of the inline coefficient, as in edge_coef_kernel -- row i's
+// w and P in registers and all 2C loads of row j in one round trip (-C exact even count, > 0 a
+// bound, 0 the generic loop: C dependent round trips per edge, which dominated the batched NS
+// gradient).  Same fma order, so every form agrees bitwise.
+template <bool AUTO, int ND, bool VEC, bool WIDE, int CV>
 __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float* __restrict__ X,
                                                         float* __restrict__ out, size_t xs,
                                                         size_t gxs) {
@@ -204,12 +208,17 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
         const int e = e0 + lane;
         float cf = 0.f;
         int cj = i;
+        // row i's w and P for the register form (fixed eps), loaded per 64 edges so they are
+        // dead during the gathers below (VGPRs = occupancy); AUTO or CV = 0: unused
+        const auto ri = row_wp<(AUTO || CV == 0) ? 1 : CV>(a, (AUTO || CV == 0) ? 0 : i);
         if (e < end) {
             cj = a.col[e];
             if constexpr (AUTO) {
                 cf = a.S[e];
                 if (cj == kth_i) cf -= b_i;
                 if (a.knn_idx[size_t(cj) * a.K + a.K - 1] == i) cf -= a.b[cj];
+            } else if constexpr (CV != 0) {
+                cf = edge_gv_r<CV>(a, ri, cj, a.w[e], ei);
             } else {
                 float g;
                 cf = edge_gv(a, i, cj, a.w[e], ei, g);
@@ -363,7 +372,7 @@ static void grad_chunked(const EdgeArgs& a, const Batch& bt, const float* X, flo
         launch_k(grad_chunk_kernel<COEF, 64>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx);
 }
 
-template <bool AUTO, bool VEC>
+template <bool AUTO, bool VEC, int CV>
 static hipError_t grad_nd(const EdgeArgs& a, const Batch& bt, const float* X, float* out,
                           hipStream_t s) {
     dim3 grid((a.n + 3) / 4, bt.B);
@@ -371,9 +380,9 @@ static hipError_t grad_nd(const EdgeArgs& a, const Batch& bt, const float* X, fl
 #define GLL_GRAD(ND)                                                                        \
     do {                                                                                    \
         if (bt.B == 1 && ND <= 4)                                                           \
-            launch_k(grad_spmm_kernel<AUTO, ND, VEC, true>, grid, 256, 0, s, a, X, out, bt.x, bt.gx);  \
+            launch_k(grad_spmm_kernel<AUTO, ND, VEC, true, CV>, grid, 256, 0, s, a, X, out, bt.x, bt.gx);  \
         else                                                                                \
-            launch_k(grad_spmm_kernel<AUTO, ND, VEC, false>, grid, 256, 0, s, a, X, out, bt.x, bt.gx); \
+            launch_k(grad_spmm_kernel<AUTO, ND, VEC, false, CV>, grid, 256, 0, s, a, X, out, bt.x, bt.gx); \
     } while (0)
     if (nd <= 1) GLL_GRAD(1);
     else if (nd <= 2) GLL_GRAD(2);
@@ -436,11 +445,19 @@ hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, cons
         else grad_chunked<2>(a, bt, X, gradX, s);
         e = launch_status("grad.hip:grad_chunked");
     } else if (auto_eps) {
-        e = vec ? grad_nd<true, true>(a, bt, X, gradX, s)
-                : grad_nd<true, false>(a, bt, X, gradX, s);
+        e = vec ? grad_nd<true, true, 0>(a, bt, X, gradX, s)
+                : grad_nd<true, false, 0>(a, bt, X, gradX, s);
     } else {
-        e = vec ? grad_nd<false, true>(a, bt, X, gradX, s)
-                : grad_nd<false, false>(a, bt, X, gradX, s);
+        // fixed eps: inline coefficient in register form (diagnostic GLL_GRAD_CV=0 keeps the
+        // generic loop, for A/B)
+        static const bool generic = getenv("GLL_GRAD_CV") && atoi(getenv("GLL_GRAD_CV")) == 0;
+        // (ten classes: every caller's label matrix, FullySup.py:153; other C the generic loop)
+        if (!generic && L.C == 10)
+            e = vec ? grad_nd<false, true, -10>(a, bt, X, gradX, s)
+                    : grad_nd<false, false, -10>(a, bt, X, gradX, s);
+        else
+            e = vec ? grad_nd<false, true, 0>(a, bt, X, gradX, s)
+                    : grad_nd<false, false, 0>(a, bt, X, gradX, s);
     }
     prof_end(GLL_K_GRAD, s);
     return e;

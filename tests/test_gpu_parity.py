@@ -514,6 +514,49 @@ def test_utils_laplace_large_graph_matches_oracle():
     assert acc == pytest.approx(100.0 * np.mean(Uo.argmax(1) == labels[250:]), abs=0.05)
 
 
+def test_utils_laplace_reference_size_properties():
+    """utils.laplace at the reference's evaluation size (250 labeled + 50,000 unlabeled train +
+    10,000 test, d = 128, k = 50, utils.py:570-593): too large for the SuperLU oracle, so
+    size-independent properties instead.  (1) kNN lists of 64 sampled rows equal the exact
+    float64 sets over all 60,250 points; (2) the reference's own stopping criterion holds in
+    float64 on the host, recomputed from the GPU graph: max_c ||M (rhs - Luu x)|| <= 1e-10 with
+    M = diag(Luu + 1e-10)^(-1/2) (utils.py:586-591, GLL.py:259); (3) every prediction row is
+    a convex combination of the labels (rows sum to 1, entries in [0, 1], maximum principle)."""
+    import scipy.sparse as sp
+    from graphlearninglayer_amd import utils as U_
+    from graphlearninglayer_amd.synth import synth
+    nl, nu, k = 250, 60000, 50
+    X, labels = synth(nl, nu, 128, C=10, r=1.0, seed=3)
+    Xd = torch.from_numpy(X).cuda()
+    U = U_.laplace(Xd, labels[:nl], knn_num=k, epsilon=1.0, tau=1e-8)
+    n, m = nl + nu, nu
+    assert U.shape == (m, 10) and np.isfinite(U).all()
+    g = _gpu_knn(X, k, 1.0)
+    ind = g["knn_idx"].cpu().numpy()
+    rng = np.random.default_rng(0)
+    X64 = X.astype(np.float64)
+    for i in rng.choice(n, 64, replace=False):
+        d2 = np.sum((X64 - X64[i]) ** 2, axis=1)
+        order = np.argsort(d2, kind="stable")
+        gap = d2[order[k]] - d2[order[k - 1]]
+        if gap > 1e-12 * max(d2[order[k]], 1e-30):     # no exact tie at the boundary
+            assert set(ind[i].tolist()) == set(order[:k].tolist()), f"row {i}"
+    rp, col = g["row_ptr"].cpu().numpy(), g["col"].cpu().numpy()
+    W = sp.csr_matrix((g["w"].cpu().numpy().astype(np.float64), col, rp), shape=(n, n))
+    deg = np.asarray(W.sum(axis=1)).ravel()
+    L = (sp.diags(deg) - W).tocsr()
+    Luu = L[nl:, nl:] + 1e-8 * sp.eye(m)
+    Y = U_.one_hot_encode(labels[:nl])
+    rhs = -(L[nl:, :nl] @ Y)
+    Mv = 1.0 / np.sqrt(Luu.diagonal() + 1e-10)
+    res = np.linalg.norm(Mv[:, None] * (rhs - Luu @ U), axis=0)
+    assert res.max() <= 2e-10, f"scaled residual {res.max():.3e}"
+    # Luu is an M-matrix and W_ul Y >= 0, so 0 <= U and U 1 = 1 - tau Luu^-1 1 <= 1
+    assert U.min() >= -1e-7 and U.sum(1).max() <= 1.0 + 1e-7
+    acc = 100.0 * np.mean(U.argmax(1) == labels[nl:])
+    print(f"n={n}: scaled residual {res.max():.2e}, GL accuracy {acc:.2f}%")
+
+
 def _exact_knn_rows(X, ind, k):
     """Rows whose GPU kNN set differs from the exact float64 set (ties at 1e-12 excused)."""
     return O.knn_set_mismatch(X, ind, k, rel_gap=1e-12)
