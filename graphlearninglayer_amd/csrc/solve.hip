@@ -201,20 +201,21 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     const float* __restrict__ ell_w, size_t wss, size_t bs,
     size_t us, size_t sts) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    ell_col = gshift<true>(ell_col, wss);
-    ell_w = gshift<true>(ell_w, wss);
-    row_start = gshift_br<true>(row_start, wss);   // batched launches: graph blockIdx.y
-    row_len = gshift_br<true>(row_len, wss);
-    ucnt = gshift<true>(ucnt, wss);
-    col = gshift_br<true>(col, wss);
-    wv = gshift_br<true>(wv, wss);
-    diag = gshift<true>(diag, wss);
-    bsrc = gshift<true>(bsrc, bs);
-    out64 = gshift_br<true>(out64, us);
-    out32 = gshift_br<true>(out32, wss);
-    st_nonconv = gshift_br<true>(st_nonconv, sts);
-    st_iters = gshift_br<true>(st_iters, sts);
-    const int c = bx<true>();
+    const int2 gxy = batch_xy<true>();   // once: per pointer it re-reads gridDim and divides
+    ell_col = gshift_at(ell_col, wss, gxy.y);
+    ell_w = gshift_at(ell_w, wss, gxy.y);
+    row_start = gshift_br_at(row_start, wss, gxy.y);   // batched launches: graph blockIdx.y
+    row_len = gshift_br_at(row_len, wss, gxy.y);
+    ucnt = gshift_at(ucnt, wss, gxy.y);
+    col = gshift_br_at(col, wss, gxy.y);
+    wv = gshift_br_at(wv, wss, gxy.y);
+    diag = gshift_at(diag, wss, gxy.y);
+    bsrc = gshift_at(bsrc, bs, gxy.y);
+    out64 = gshift_br_at(out64, us, gxy.y);
+    out32 = gshift_br_at(out32, wss, gxy.y);
+    st_nonconv = gshift_br_at(st_nonconv, sts, gxy.y);
+    st_iters = gshift_br_at(st_iters, sts, gxy.y);
+    const int c = gxy.x;
     const int tid = threadIdx.x;
     float* red = smem;                                  // 96 floats of reduction scratch
     int* scan = reinterpret_cast<int*>(smem + 96);      // 16 ints of scan scratch
@@ -668,20 +669,21 @@ __global__ __launch_bounds__(NT) void cg_vr_kernel(
     float* __restrict__ out32, float rtol, int max_iter, int32_t* __restrict__ st_nonconv,
     int32_t* __restrict__ st_iters, size_t wss, size_t bs, size_t us, size_t sts) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    row_start = gshift<true>(row_start, wss);
-    row_len = gshift<true>(row_len, wss);
-    ucnt = gshift<true>(ucnt, wss);
-    col = gshift<true>(col, wss);
-    wv = gshift<true>(wv, wss);
-    diag = gshift<true>(diag, wss);
-    vrs = gshift<true>(vrs, wss);
-    bsrc = gshift<true>(bsrc, bs);
-    out64 = gshift_br<true>(out64, us);
-    out32 = gshift_br<true>(out32, wss);
-    st_nonconv = gshift_br<true>(st_nonconv, sts);
-    st_iters = gshift_br<true>(st_iters, sts);
+    const int2 gxy = batch_xy<true>();   // once: per pointer it re-reads gridDim and divides
+    row_start = gshift_at(row_start, wss, gxy.y);
+    row_len = gshift_at(row_len, wss, gxy.y);
+    ucnt = gshift_at(ucnt, wss, gxy.y);
+    col = gshift_at(col, wss, gxy.y);
+    wv = gshift_at(wv, wss, gxy.y);
+    diag = gshift_at(diag, wss, gxy.y);
+    vrs = gshift_at(vrs, wss, gxy.y);
+    bsrc = gshift_at(bsrc, bs, gxy.y);
+    out64 = gshift_br_at(out64, us, gxy.y);
+    out32 = gshift_br_at(out32, wss, gxy.y);
+    st_nonconv = gshift_br_at(st_nonconv, sts, gxy.y);
+    st_iters = gshift_br_at(st_iters, sts, gxy.y);
     constexpr int VCAP = NT * RV;
-    const int c = bx<true>();
+    const int c = gxy.x;
     const int tid = threadIdx.x;
     const int mp4 = (m + 3) & ~3;
     float* red = smem;                                   // 96 floats of reduction scratch
@@ -953,19 +955,20 @@ __global__ __launch_bounds__(NT) void cg_lds_kernel(
     float* __restrict__ gvec, int vec_in_lds, int32_t* __restrict__ st_nonconv,
     int32_t* __restrict__ st_iters, size_t wss, size_t bs, size_t us, size_t sts) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    row_start = gshift<true>(row_start, wss);
-    row_len = gshift<true>(row_len, wss);
-    ucnt = gshift<true>(ucnt, wss);
-    col = gshift<true>(col, wss);
-    wv = gshift<true>(wv, wss);
-    diag = gshift<true>(diag, wss);
-    bsrc = gshift<true>(bsrc, bs);
-    out64 = gshift<true>(out64, us);
-    out32 = gshift<true>(out32, wss);
-    gvec = gshift<true>(gvec, wss);
-    st_nonconv = gshift<true>(st_nonconv, sts);
-    st_iters = gshift<true>(st_iters, sts);
-    const int c = bx<true>();
+    const int2 gxy = batch_xy<true>();   // once: per pointer it re-reads gridDim and divides
+    row_start = gshift_at(row_start, wss, gxy.y);
+    row_len = gshift_at(row_len, wss, gxy.y);
+    ucnt = gshift_at(ucnt, wss, gxy.y);
+    col = gshift_at(col, wss, gxy.y);
+    wv = gshift_at(wv, wss, gxy.y);
+    diag = gshift_at(diag, wss, gxy.y);
+    bsrc = gshift_at(bsrc, bs, gxy.y);
+    out64 = gshift_at(out64, us, gxy.y);
+    out32 = gshift_at(out32, wss, gxy.y);
+    gvec = gshift_at(gvec, wss, gxy.y);
+    st_nonconv = gshift_at(st_nonconv, sts, gxy.y);
+    st_iters = gshift_at(st_iters, sts, gxy.y);
+    const int c = gxy.x;
     const int tid = threadIdx.x;
     float* red = smem;
     float* vb = vec_in_lds ? smem + 64 : gvec + size_t(c) * 5 * m;
