@@ -409,11 +409,32 @@ __device__ __forceinline__ int bg() { return batch_xy<R>().y; }
 // Branch-free on purpose: a branch per pointer splits the prologue into basic blocks with an
 // s_waitcnt each, serialising the kernel-argument loads (~13 dependent scalar loads, ~0.5 us
 // at the start of every kernel); selects let them all be in flight at once.
+// Pointer (not integer) arithmetic: an integer round trip loses the pointer's provenance, and
+// with it the compiler's proof that it points to global memory -- every access through it
+// became a flat instruction (no scalar base, waits on both the vector and LDS counters).
 template <bool R = false, typename T>
 __device__ __forceinline__ T* gshift(T* p, size_t stride) {
+    using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+    const size_t off = size_t(bg<R>()) * stride;
+    return reinterpret_cast<T*>(reinterpret_cast<B*>(p) + (p != nullptr ? off : size_t(0)));
+}
+
+// Integer-arithmetic form: the result is a generic (flat) pointer to the compiler.  Kept for
+// kernels where flat accesses measured faster (see its users).
+template <bool R = false, typename T>
+__device__ __forceinline__ T* gshift_flat(T* p, size_t stride) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     const uintptr_t off = uintptr_t(bg<R>()) * stride;
     return reinterpret_cast<T*>(a + (a != 0 ? off : uintptr_t(0)));
+}
+
+// The same with the graph index already known (a kernel shifting many pointers computes
+// batch_xy once: per pointer, the batched numbering re-reads gridDim and divides each time).
+template <typename T>
+__device__ __forceinline__ T* gshift_at(T* p, size_t stride, int g) {
+    using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+    const size_t off = size_t(g) * stride;
+    return reinterpret_cast<T*>(reinterpret_cast<B*>(p) + (p != nullptr ? off : size_t(0)));
 }
 
 // Branching form for the register-tight Gram kernels (four pointers, no long load chain):
@@ -423,6 +444,13 @@ __device__ __forceinline__ T* gshift_br(T* p, size_t stride) {
     if (p == nullptr || stride == 0) return p;
     using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
     return reinterpret_cast<T*>(reinterpret_cast<B*>(p) + size_t(bg<R>()) * stride);
+}
+
+template <typename T>
+__device__ __forceinline__ T* gshift_br_at(T* p, size_t stride, int g) {
+    if (p == nullptr || stride == 0) return p;
+    using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+    return reinterpret_cast<T*>(reinterpret_cast<B*>(p) + size_t(g) * stride);
 }
 
 // Launch-error report (GLL_DEBUG=1 in the environment): which launcher failed and why.

@@ -35,18 +35,19 @@ struct EdgeArgs {
     size_t wss;           // batched launches: workspace stride between graphs (bytes)
 
     template <bool R = false>
-    __device__ void to_graph() {   // move every workspace pointer to this block's graph
-        row_start = gshift<R>(row_start, wss);
-        row_len = gshift<R>(row_len, wss);
-        col = gshift<R>(col, wss);
-        w = gshift<R>(w, wss);
-        d2 = gshift<R>(d2, wss);
-        eps = gshift<R>(eps, wss);
-        P = gshift<R>(P, wss);
-        Wadj = gshift<R>(Wadj, wss);
-        knn_idx = gshift<R>(knn_idx, wss);
-        S = gshift<R>(S, wss);
-        b = gshift<R>(b, wss);
+    __device__ void to_graph() { to_graph_at(bg<R>()); }
+    __device__ void to_graph_at(int g) {   // move every workspace pointer to graph g
+        row_start = gshift_at(row_start, wss, g);
+        row_len = gshift_at(row_len, wss, g);
+        col = gshift_at(col, wss, g);
+        w = gshift_at(w, wss, g);
+        d2 = gshift_at(d2, wss, g);
+        eps = gshift_at(eps, wss, g);
+        P = gshift_at(P, wss, g);
+        Wadj = gshift_at(Wadj, wss, g);
+        knn_idx = gshift_at(knn_idx, wss, g);
+        S = gshift_at(S, wss, g);
+        b = gshift_at(b, wss, g);
     }
 };
 
@@ -181,11 +182,12 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
                                                         float* __restrict__ out, size_t xs,
                                                         size_t gxs) {
     GLL_TRACE_SCOPE(1);
-    a.to_graph<true>();
-    X = gshift<true>(X, xs);
-    out = gshift<true>(out, gxs);
+    const int2 xy = batch_xy<true>();   // once: (block within the graph, graph)
+    a.to_graph_at(xy.y);
+    X = gshift_at(X, xs, xy.y);
+    out = gshift_at(out, gxs, xy.y);
     const int lane = lane_id();
-    const int i = bx<true>() * 4 + (threadIdx.x >> 6);
+    const int i = xy.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
     const int d = a.d;
     const int beg = a.row_start[i], end = beg + a.row_len[i];

@@ -57,31 +57,32 @@ struct RowArgs {
     int VRM;
     size_t wss;   // batched launches: workspace stride between graphs (bytes)
 
+    template <bool FLAT>
     __device__ void to_graph() {   // move every workspace pointer to graph blockIdx.y
-        knn_idx = gshift(knn_idx, wss);
-        knn_d2 = gshift(knn_d2, wss);
-        rev_cnt = gshift(rev_cnt, wss);
-        rev_idx = gshift(rev_idx, wss);
-        rev_d2 = gshift(rev_d2, wss);
-        ovf = gshift(ovf, wss);
-        status = gshift(status, wss);
-        eps = gshift(eps, wss);
-        tmp_col = gshift(tmp_col, wss);
-        tmp_d2 = gshift(tmp_d2, wss);
-        row_start = gshift(row_start, wss);
-        row_len = gshift(row_len, wss);
-        col = gshift(col, wss);
-        w = gshift(w, wss);
-        d2e = gshift(d2e, wss);
-        deg = gshift(deg, wss);
-        ucnt = gshift(ucnt, wss);
-        diag = gshift(diag, wss);
-        rhs = gshift(rhs, wss);
-        P = gshift(P, wss);
-        Wadj = gshift(Wadj, wss);
-        ell_col = gshift(ell_col, wss);
-        ell_w = gshift(ell_w, wss);
-        vr = gshift(vr, wss);
+        knn_idx = FLAT ? gshift_flat(knn_idx, wss) : gshift(knn_idx, wss);
+        knn_d2 = FLAT ? gshift_flat(knn_d2, wss) : gshift(knn_d2, wss);
+        rev_cnt = FLAT ? gshift_flat(rev_cnt, wss) : gshift(rev_cnt, wss);
+        rev_idx = FLAT ? gshift_flat(rev_idx, wss) : gshift(rev_idx, wss);
+        rev_d2 = FLAT ? gshift_flat(rev_d2, wss) : gshift(rev_d2, wss);
+        ovf = FLAT ? gshift_flat(ovf, wss) : gshift(ovf, wss);
+        status = FLAT ? gshift_flat(status, wss) : gshift(status, wss);
+        eps = FLAT ? gshift_flat(eps, wss) : gshift(eps, wss);
+        tmp_col = FLAT ? gshift_flat(tmp_col, wss) : gshift(tmp_col, wss);
+        tmp_d2 = FLAT ? gshift_flat(tmp_d2, wss) : gshift(tmp_d2, wss);
+        row_start = FLAT ? gshift_flat(row_start, wss) : gshift(row_start, wss);
+        row_len = FLAT ? gshift_flat(row_len, wss) : gshift(row_len, wss);
+        col = FLAT ? gshift_flat(col, wss) : gshift(col, wss);
+        w = FLAT ? gshift_flat(w, wss) : gshift(w, wss);
+        d2e = FLAT ? gshift_flat(d2e, wss) : gshift(d2e, wss);
+        deg = FLAT ? gshift_flat(deg, wss) : gshift(deg, wss);
+        ucnt = FLAT ? gshift_flat(ucnt, wss) : gshift(ucnt, wss);
+        diag = FLAT ? gshift_flat(diag, wss) : gshift(diag, wss);
+        rhs = FLAT ? gshift_flat(rhs, wss) : gshift(rhs, wss);
+        P = FLAT ? gshift_flat(P, wss) : gshift(P, wss);
+        Wadj = FLAT ? gshift_flat(Wadj, wss) : gshift(Wadj, wss);
+        ell_col = FLAT ? gshift_flat(ell_col, wss) : gshift(ell_col, wss);
+        ell_w = FLAT ? gshift_flat(ell_w, wss) : gshift(ell_w, wss);
+        vr = FLAT ? gshift_flat(vr, wss) : gshift(vr, wss);
     }
 };
 
@@ -301,11 +302,11 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
 
 // PRE: label prefetch (single-graph launches; its 20 KiB of LDS halves the workgroups per CU
 // that batches need: B = 64 NS 72 -> 90 us with it)
-template <typename TY, bool PRE>
+template <typename TY, bool PRE, bool FLAT>
 __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __restrict__ Y,
                                                         size_t ys) {
     GLL_TRACE_SCOPE(0);
-    a.to_graph();
+    a.to_graph<FLAT>();
     Y = gshift(Y, ys);
     __shared__ int s_col[4][kStage];
     __shared__ float s_d2[4][kStage];
@@ -394,12 +395,16 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     a.wss = bt.ws;
     dim3 grid((L.n + 3) / 4, bt.B);
     prof_begin(GLL_K_FINALIZE, s);
+    // Batched launches address the workspace through flat pointers (integer-shifted, so the
+    // compiler cannot prove them global): measured faster there (NS B = 64 68 -> 63 us, FullySup
+    // B = 64 127 -> 116 us, profiles/r02h_rows_flat_ab.txt), while the single-graph kernel is
+    // as fast or faster with global loads (6.5 -> 6.4 us).
 #define GLL_ROWS(T)                                                                          \
     do {                                                                                     \
         if (bt.B == 1)                                                                       \
-            launch_k(row_build_kernel<T, true>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y);  \
+            launch_k(row_build_kernel<T, true, false>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y);  \
         else                                                                                 \
-            launch_k(row_build_kernel<T, false>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y); \
+            launch_k(row_build_kernel<T, false, true>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y); \
     } while (0)
     if (y_dtype == GLL_DT_F32) GLL_ROWS(float);
     else if (y_dtype == GLL_DT_F64) GLL_ROWS(double);
