@@ -399,8 +399,10 @@ __device__ __forceinline__ int2 batch_xy() {
 }
 // R = true only where it measured faster (tools/ab_flags.py, B = 64 / 8): the per-column CG
 // (NS B = 64 32 -> 24 us, stress B = 64 2.0 -> 1.1 ms) and the whole-row feature gradient (NS
-// B = 64 198 -> 178 us, FullySup B = 64 347 -> 305 us).  Row build (NS B = 64 60 -> 170 us) and
-// select (251 -> 292 us) ran slower with it, and the chunked gradient needs block % 8 = chunk.
+// B = 64 198 -> 178 us, FullySup B = 64 347 -> 305 us), and -- once kernels took batch_xy once
+// instead of per pointer (gshift_at) -- the select (NS B = 64 220 -> 213 us).  The row build
+// still runs slower with it (62 -> 66 us), and the chunked gradient needs block % 8 = chunk.
+// A kernel computes batch_xy ONCE: per call it re-reads gridDim and divides.
 template <bool R = false>
 __device__ __forceinline__ int bx() { return batch_xy<R>().x; }
 template <bool R = false>
@@ -420,11 +422,11 @@ __device__ __forceinline__ T* gshift(T* p, size_t stride) {
 }
 
 // Integer-arithmetic form: the result is a generic (flat) pointer to the compiler.  Kept for
-// kernels where flat accesses measured faster (see its users).
-template <bool R = false, typename T>
-__device__ __forceinline__ T* gshift_flat(T* p, size_t stride) {
+// the batched row build, where flat accesses measured faster (rows.hip launch_finalize).
+template <typename T>
+__device__ __forceinline__ T* gshift_flat_at(T* p, size_t stride, int g) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uintptr_t off = uintptr_t(bg<R>()) * stride;
+    const uintptr_t off = uintptr_t(g) * stride;
     return reinterpret_cast<T*>(a + (a != 0 ? off : uintptr_t(0)));
 }
 

@@ -1243,24 +1243,25 @@ void knn_select_kernel(
     size_t sts) {
     GLL_TRACE_SCOPE(1);
     GLL_TRACE_PT(20);
-    D2 = gshift<R>(D2, wss);
-    X = gshift<R>(X, xs);
-    knn_idx = gshift<R>(knn_idx, wss);
-    knn_d2 = gshift<R>(knn_d2, wss);
-    eps = gshift<R>(eps, wss);
-    rev_cnt = gshift<R>(rev_cnt, wss);
-    rev_idx = gshift<R>(rev_idx, wss);
-    rev_d2 = gshift<R>(rev_d2, wss);
-    ovf = gshift<R>(ovf, wss);
-    status = gshift<R>(status, wss);
-    status_pub = gshift<R>(status_pub, sts);
+    const int2 gxy = batch_xy<R>();   // once (per pointer it re-reads gridDim and divides)
+    D2 = gshift_at(D2, wss, gxy.y);
+    X = gshift_at(X, xs, gxy.y);
+    knn_idx = gshift_at(knn_idx, wss, gxy.y);
+    knn_d2 = gshift_at(knn_d2, wss, gxy.y);
+    eps = gshift_at(eps, wss, gxy.y);
+    rev_cnt = gshift_at(rev_cnt, wss, gxy.y);
+    rev_idx = gshift_at(rev_idx, wss, gxy.y);
+    rev_d2 = gshift_at(rev_d2, wss, gxy.y);
+    ovf = gshift_at(ovf, wss, gxy.y);
+    status = gshift_at(status, wss, gxy.y);
+    status_pub = gshift_at(status_pub, sts, gxy.y);
     __shared__ int s_cand[4][kWave];
     __shared__ uint32_t s_cgd[4][kWave];
     constexpr bool XL = XQ > 0;
     __shared__ float s_xi[XL ? 4 : 1][XL ? 256 * XQ : 1];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
-    const int i = bx<R>() * 4 + wv;
+    const int i = gxy.x * 4 + wv;
     if (i >= n) return;  // whole wave
     // XL: x_i is staged once in LDS (its loads ride under the D2 scan's), so the exact
     // distances hold only the candidates' rows in registers (occupancy) and do not re-load x_i
@@ -1527,9 +1528,12 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
 // batch of loads held 120 VGPRs, 4 waves).  NU: 32-feature steps per exact-distance load batch,
 // d / 32 up to 8 for batches (16 for single graphs, whose one wave per SIMD has registers to
 // spare); the loads of steps past d are clamped to row 0 and masked.
+// Batched launches number blocks XCD-contiguously (R = true: each XCD works through a run of
+// graphs): NS B = 64 220 -> 213 us, FullySup B = 64 440 -> 429 us (profiles/r02h_xcd_ab.txt),
+// once the kernel took its graph index once instead of per pointer.
 #define GLL_SEL4(KCV, V, NPV, NUS, NUB, XQV)                                                   \
     launch_k((bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2, NUS>                               \
-                        : knn_select_kernel<KCV, V, NPV, 1, NUB, (V ? XQV : 0)>), grid, 256, 0, s, \
+                        : knn_select_kernel<KCV, V, NPV, 1, NUB, (V ? XQV : 0), true>), grid, 256, 0, s, \
         L.at<float>(ws, L.D2), L.ldD, plane, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0,     \
         L.RCAP,                                                                                \
         L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \

@@ -58,31 +58,31 @@ struct RowArgs {
     size_t wss;   // batched launches: workspace stride between graphs (bytes)
 
     template <bool FLAT>
-    __device__ void to_graph() {   // move every workspace pointer to graph blockIdx.y
-        knn_idx = FLAT ? gshift_flat(knn_idx, wss) : gshift(knn_idx, wss);
-        knn_d2 = FLAT ? gshift_flat(knn_d2, wss) : gshift(knn_d2, wss);
-        rev_cnt = FLAT ? gshift_flat(rev_cnt, wss) : gshift(rev_cnt, wss);
-        rev_idx = FLAT ? gshift_flat(rev_idx, wss) : gshift(rev_idx, wss);
-        rev_d2 = FLAT ? gshift_flat(rev_d2, wss) : gshift(rev_d2, wss);
-        ovf = FLAT ? gshift_flat(ovf, wss) : gshift(ovf, wss);
-        status = FLAT ? gshift_flat(status, wss) : gshift(status, wss);
-        eps = FLAT ? gshift_flat(eps, wss) : gshift(eps, wss);
-        tmp_col = FLAT ? gshift_flat(tmp_col, wss) : gshift(tmp_col, wss);
-        tmp_d2 = FLAT ? gshift_flat(tmp_d2, wss) : gshift(tmp_d2, wss);
-        row_start = FLAT ? gshift_flat(row_start, wss) : gshift(row_start, wss);
-        row_len = FLAT ? gshift_flat(row_len, wss) : gshift(row_len, wss);
-        col = FLAT ? gshift_flat(col, wss) : gshift(col, wss);
-        w = FLAT ? gshift_flat(w, wss) : gshift(w, wss);
-        d2e = FLAT ? gshift_flat(d2e, wss) : gshift(d2e, wss);
-        deg = FLAT ? gshift_flat(deg, wss) : gshift(deg, wss);
-        ucnt = FLAT ? gshift_flat(ucnt, wss) : gshift(ucnt, wss);
-        diag = FLAT ? gshift_flat(diag, wss) : gshift(diag, wss);
-        rhs = FLAT ? gshift_flat(rhs, wss) : gshift(rhs, wss);
-        P = FLAT ? gshift_flat(P, wss) : gshift(P, wss);
-        Wadj = FLAT ? gshift_flat(Wadj, wss) : gshift(Wadj, wss);
-        ell_col = FLAT ? gshift_flat(ell_col, wss) : gshift(ell_col, wss);
-        ell_w = FLAT ? gshift_flat(ell_w, wss) : gshift(ell_w, wss);
-        vr = FLAT ? gshift_flat(vr, wss) : gshift(vr, wss);
+    __device__ void to_graph(int g) {   // move every workspace pointer to graph g
+        knn_idx = FLAT ? gshift_flat_at(knn_idx, wss, g) : gshift_at(knn_idx, wss, g);
+        knn_d2 = FLAT ? gshift_flat_at(knn_d2, wss, g) : gshift_at(knn_d2, wss, g);
+        rev_cnt = FLAT ? gshift_flat_at(rev_cnt, wss, g) : gshift_at(rev_cnt, wss, g);
+        rev_idx = FLAT ? gshift_flat_at(rev_idx, wss, g) : gshift_at(rev_idx, wss, g);
+        rev_d2 = FLAT ? gshift_flat_at(rev_d2, wss, g) : gshift_at(rev_d2, wss, g);
+        ovf = FLAT ? gshift_flat_at(ovf, wss, g) : gshift_at(ovf, wss, g);
+        status = FLAT ? gshift_flat_at(status, wss, g) : gshift_at(status, wss, g);
+        eps = FLAT ? gshift_flat_at(eps, wss, g) : gshift_at(eps, wss, g);
+        tmp_col = FLAT ? gshift_flat_at(tmp_col, wss, g) : gshift_at(tmp_col, wss, g);
+        tmp_d2 = FLAT ? gshift_flat_at(tmp_d2, wss, g) : gshift_at(tmp_d2, wss, g);
+        row_start = FLAT ? gshift_flat_at(row_start, wss, g) : gshift_at(row_start, wss, g);
+        row_len = FLAT ? gshift_flat_at(row_len, wss, g) : gshift_at(row_len, wss, g);
+        col = FLAT ? gshift_flat_at(col, wss, g) : gshift_at(col, wss, g);
+        w = FLAT ? gshift_flat_at(w, wss, g) : gshift_at(w, wss, g);
+        d2e = FLAT ? gshift_flat_at(d2e, wss, g) : gshift_at(d2e, wss, g);
+        deg = FLAT ? gshift_flat_at(deg, wss, g) : gshift_at(deg, wss, g);
+        ucnt = FLAT ? gshift_flat_at(ucnt, wss, g) : gshift_at(ucnt, wss, g);
+        diag = FLAT ? gshift_flat_at(diag, wss, g) : gshift_at(diag, wss, g);
+        rhs = FLAT ? gshift_flat_at(rhs, wss, g) : gshift_at(rhs, wss, g);
+        P = FLAT ? gshift_flat_at(P, wss, g) : gshift_at(P, wss, g);
+        Wadj = FLAT ? gshift_flat_at(Wadj, wss, g) : gshift_at(Wadj, wss, g);
+        ell_col = FLAT ? gshift_flat_at(ell_col, wss, g) : gshift_at(ell_col, wss, g);
+        ell_w = FLAT ? gshift_flat_at(ell_w, wss, g) : gshift_at(ell_w, wss, g);
+        vr = FLAT ? gshift_flat_at(vr, wss, g) : gshift_at(vr, wss, g);
     }
 };
 
@@ -302,12 +302,13 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
 
 // PRE: label prefetch (single-graph launches; its 20 KiB of LDS halves the workgroups per CU
 // that batches need: B = 64 NS 72 -> 90 us with it)
-template <typename TY, bool PRE, bool FLAT>
+template <typename TY, bool PRE, bool FLAT, bool R = false>
 __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __restrict__ Y,
                                                         size_t ys) {
     GLL_TRACE_SCOPE(0);
-    a.to_graph<FLAT>();
-    Y = gshift(Y, ys);
+    const int2 gxy = batch_xy<R>();   // once (per pointer it re-reads gridDim and divides)
+    a.to_graph<FLAT>(gxy.y);
+    Y = gshift_at(Y, ys, gxy.y);
     __shared__ int s_col[4][kStage];
     __shared__ float s_d2[4][kStage];
     __shared__ int t_col[4][kStage];
@@ -317,7 +318,7 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
     __shared__ float ybuf[4][PRE ? kWave * kYPre : 1];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
-    const int i = bx() * 4 + wv;
+    const int i = gxy.x * 4 + wv;
     if (i >= a.n) return;
     const int Km1 = a.K - 1;
     int fi = -1;
@@ -398,7 +399,9 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     // Batched launches address the workspace through flat pointers (integer-shifted, so the
     // compiler cannot prove them global): measured faster there (NS B = 64 68 -> 63 us, FullySup
     // B = 64 127 -> 116 us, profiles/r02h_rows_flat_ab.txt), while the single-graph kernel is
-    // as fast or faster with global loads (6.5 -> 6.4 us).
+    // as fast or faster with global loads (6.5 -> 6.4 us).  XCD-contiguous numbering (R) measured
+    // slower here even with the graph index taken once (NS B = 64 62 -> 66 us, FullySup B = 64
+    // 116 -> 125 us, profiles/r02h_xcd_ab.txt).
 #define GLL_ROWS(T)                                                                          \
     do {                                                                                     \
         if (bt.B == 1)                                                                       \
