@@ -1467,9 +1467,13 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
     // a single NS graph has only 36); 64-tiles otherwise
     const int T = (L.n + 127) / 128;
     // pre-split GEMM from 256 tiles (NS B = 8, 288 tiles: 58 -> 45 us; a single FullySup graph,
-    // 78 tiles, stays on the 64-tile kernel: 17.5 against 21.6 us)
+    // 78 tiles, stays on the 64-tile kernel: 17.5 against 21.6 us).  Not for single graphs with
+    // d <= 128 (utils.laplace's 250 + 60,000 points: one K stage, nothing for the DMA pipeline to
+    // hide, and the whole graph build took 166 ms with it against 19 ms with the inline 128-tile
+    // kernel; 20,250 points 3.9 -> 2.1 ms; profiles/r02i_gram_inline_ab.txt).  Batches
+    // and d = 1024 keep it (NS B = 64 322 -> 237 us, FullySup B = 64 272 -> 228, stress 485 -> 319).
     if (!(L.flags & GLL_FLAG_GRAM_NARROW) && int64_t(bt.B) * T * (T + 1) / 2 >= 256 &&
-        !(L.flags & GLL_FLAG_GRAM_INLINE)) {
+        !(L.flags & GLL_FLAG_GRAM_INLINE) && !(bt.B == 1 && L.d <= 128)) {
         // split once (one pass over X), then the LDS-DMA bf16 GEMM over 128-tiles
         __bf16* Ph = L.at<__bf16>(ws, L.xhi);
         __bf16* Pl = L.at<__bf16>(ws, L.xlo);

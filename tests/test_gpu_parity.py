@@ -757,18 +757,32 @@ def test_chunked_grad_matches_row_kernel_bitwise(cfg, eps):
 @pytest.mark.parametrize("d", [100, 37, 256])
 def test_presplit_gram_matches_inline_split(d):
     """The 128-tile Gram on pre-split hi/lo planes with LDS-DMA staging (knn.hip gram_split_kernel
-    + gram_pk_kernel, the default for large graphs and batches) against the inline-split kernel
-    (GLL_FLAG_GRAM_INLINE): both only nominate candidates, so the kNN (exact against float64)
-    and every output agree bitwise; ragged n (not a multiple of 128) and d (not of 64, and not
-    of 4: the scalar load path)."""
+    + gram_pk_kernel, the default for batches and for large graphs with d > 128) against the
+    inline-split kernel (GLL_FLAG_GRAM_INLINE): both only nominate candidates, so the kNN (exact
+    against float64) and every output agree bitwise; ragged n (not a multiple of 128) and d (not
+    of 64, and not of 4: the scalar load path).  For d <= 128 the pre-split path runs batched."""
     from graphlearninglayer_amd import _lib
     from graphlearninglayer_amd.synth import one_hot, synth
     base, m, k = 1000, 3037, 10   # 32 128-row tiles a side: 528 tiles, the 128-tile path
     X, lab = synth(base, m, d, r=1.0, seed=8)
     Y = one_hot(lab[:base])
-    Up, itp, ncp = _forward_c_abi(X, Y, k, 0.07, "auto")
     Ui, iti, nci = _forward_c_abi(X, Y, k, 0.07, "auto", flags=_lib.FLAG_GRAM_INLINE)
-    assert ncp == 0 and nci == 0
-    np.testing.assert_array_equal(Up, Ui)
+    assert nci == 0
     ind = _gpu_knn(X, k, "auto")["knn_idx"].cpu().numpy()
     assert _exact_knn_rows(X, ind, k) == []
+    if d > 128:
+        Up, itp, ncp = _forward_c_abi(X, Y, k, 0.07, "auto")
+        assert ncp == 0
+        np.testing.assert_array_equal(Up, Ui)
+        return
+    # single graphs with d <= 128 take the inline kernel (knn.hip launch_gram); batches keep the
+    # pre-split one: a batch of two (this graph and a second) against the single calls, at the
+    # batched-parity bar (the batched launch runs a different CG configuration)
+    GLL = _gll()
+    X2, lab2 = synth(base, m, d, r=1.0, seed=9)
+    Xb = torch.from_numpy(np.stack([X, X2])).cuda()
+    Yb = torch.from_numpy(np.stack([Y, one_hot(lab2[:base])])).cuda()
+    Ub = GLL.LaplaceLearningSparseHard.apply(Xb, Yb, 0.07, "auto", k).cpu().numpy()
+    assert O.rel_err(Ub[0], Ui) <= 1e-5
+    U2, _, _ = _forward_c_abi(X2, one_hot(lab2[:base]), k, 0.07, "auto")
+    assert O.rel_err(Ub[1], U2) <= 1e-5
