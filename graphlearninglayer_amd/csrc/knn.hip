@@ -1472,8 +1472,12 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
     // hide, and the whole graph build took 166 ms with it against 19 ms with the inline 128-tile
     // kernel; 20,250 points 3.9 -> 2.1 ms; profiles/r02i_gram_inline_ab.txt).  Batches
     // and d = 1024 keep it (NS B = 64 322 -> 237 us, FullySup B = 64 272 -> 228, stress 485 -> 319).
+    // Nor for single graphs past ~12k rows at any d: forward 5.2 vs 3.8 ms at 20,250 x 256, 16.3 vs
+    // 8.7 ms at 30,250 x 512, 17.5 vs 11.4 ms at 30,250 x 1024 (tools/gram_route_probe.py,
+    // profiles/r02j_gram_route.txt); the stress shape (8,192 x 1024) is the largest measured where
+    // it wins, and the 12,288 cut between the two is not measured.
     if (!(L.flags & GLL_FLAG_GRAM_NARROW) && int64_t(bt.B) * T * (T + 1) / 2 >= 256 &&
-        !(L.flags & GLL_FLAG_GRAM_INLINE) && !(bt.B == 1 && L.d <= 128)) {
+        !(L.flags & GLL_FLAG_GRAM_INLINE) && (bt.B > 1 || (L.d > 128 && L.n <= 12288))) {
         // split once (one pass over X), then the LDS-DMA bf16 GEMM over 128-tiles
         __bf16* Ph = L.at<__bf16>(ws, L.xhi);
         __bf16* Pl = L.at<__bf16>(ws, L.xlo);
