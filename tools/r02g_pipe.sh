@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-2g session (GPU box): batched build pipeline A/B (GLL_PIPE_CHUNKS 1/2/4 at NS, FullySup
-# and stress B = 64 / 8), then the GPU tests.  Every GPU step has its own limit; any failure ends it.
+# and stress B = 64 / 8), then the GPU tests.  The pipeline and its GLL_PIPE_CHUNKS switch were
+# removed after this measurement (slower at every chunk count); kept as the record.  Every GPU step has its own limit; any failure ends it.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out
 set -o pipefail
 run() {  # run <name> <seconds> <cmd...>
