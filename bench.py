@@ -98,17 +98,45 @@ def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps):
     n, d, K, m, C = cfg["n"], cfg["d"], cfg["k"], cfg["batch"], 10
     E, nnz_uu = graph_stats
     b_spmv = 8 * nnz_uu + 8 * m + 8 * m * C
-    cg_iter = b_spmv + 28 * m * C
     u = {
         "gram_d2_kernel": ("mfma", 2.0 * n * n * d),
         "knn_select_kernel": ("hbm", 4.0 * n * n + 8.0 * n * K),
         "row_build_kernel": ("hbm", 16.0 * E + 8.0 * n * K + 4 * n + 4 * m * C),
-        "cg_kernel": ("hbm", 0.5 * (iters_fwd + iters_bwd) * cg_iter),
+        # SURVEY §8d SpMV roofline: B_spmv per iteration (the matrix and one gathered vector);
+        # the call roofline prices a whole CG iteration instead (cg_iteration_bytes)
+        "cg_kernel": ("hbm", 0.5 * (iters_fwd + iters_bwd) * b_spmv),
         "edge_coef_kernel": ("hbm", 16.0 * E + 8.0 * n * C),
         "grad_spmm_kernel": ("hbm", (12.0 * E + 8.0 * n * d) if auto_eps
                              else (8.0 * E + 8.0 * n * C + 8.0 * n * d)),
     }
     return u
+
+
+def cg_iteration_bytes(cfg, graph_stats, iters_fwd, iters_bwd):
+    """§8d's whole CG iteration, B_spmv + 28 mC: the SpMV plus the vector updates (x, r, p, z
+    read/written once each), which this library keeps in registers and LDS -- an 'effective'
+    figure, reported beside the SpMV roofline and used by the call roofline."""
+    m, C = cfg["batch"], 10
+    _, nnz_uu = graph_stats
+    b_spmv = 8 * nnz_uu + 8 * m + 8 * m * C
+    return 0.5 * (iters_fwd + iters_bwd) * (b_spmv + 28 * m * C)
+
+
+def cg_roofline_extras(work_spmv, work_iter, avg_s, traffic):
+    """Labelled companions of the SpMV roofline of one CG launch."""
+    out = {"effective_incl_vector_bytes": {
+        "work_per_launch": work_iter,
+        "achieved_GBs": round(work_iter / avg_s / 1e9, 3),
+        "frac": round(work_iter / avg_s / 1e9 / HBM_PEAK_GBS, 5),
+        "note": "SURVEY §8d 'one CG iteration' bytes (B_spmv + 28 mC): counts the vector "
+                "updates, which live in registers / LDS here, so this overstates HBM use"}}
+    if traffic:
+        out["pmc_traffic"] = {"bytes_per_launch": traffic,
+                              "GBs": round(traffic / avg_s / 1e9, 3),
+                              "frac": round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 5),
+                              "note": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch "
+                                      "(committed PMC pass) over the live launch time"}
+    return out
 
 
 # C-ABI kernel ids (gll_kernel_name) -> device symbols as rocprofv3 names them
@@ -164,7 +192,7 @@ def gram_mfma_pmc(config):
     return None
 
 
-def batched_measure(c, eps, tau, k, B, units, dev, rank, steps=20, warmup=5):
+def batched_measure(c, eps, tau, k, B, units, cg_iter_work, dev, rank, steps=20, warmup=5):
     """B independent graphs of the workload per call of the batched entry point (X: B x n x d):
     whole-batch fwd+bwd throughput, and the CG kernel against the HBM roofline, where one
     launch now carries B graphs' SpMVs ('reported at batched NS')."""
@@ -199,17 +227,21 @@ def batched_measure(c, eps, tau, k, B, units, dev, rank, steps=20, warmup=5):
     bound, work = units["cg_kernel"]
     avg_s = ms / cnt / 1e3
     achieved = B * work / avg_s / 1e9
+    traffic = pmc_traffic(f"{c['name']}_b{B}", "cg_kernel")
+    roof = {"kernel": "cg_kernel", "bound": bound,
+            "definition": "SURVEY §8d SpMV roofline: B_spmv x iterations x B graphs / CG launch "
+                          "time / 8 TB/s, B_spmv = 8 nnz_off(Luu) + 8 m + 8 m C",
+            "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "spmv_frac": round(achieved / HBM_PEAK_GBS, 5),
+            "work_per_launch": B * work, "avg_launch_us": round(avg_s * 1e6, 3),
+            "launches": cnt, "traffic": traffic,
+            "rocprof_stats": _newest_profile(f"*_{c['name']}_b{B}_kernel_stats.csv")}
+    roof.update(cg_roofline_extras(B * work, B * cg_iter_work, avg_s, traffic))
     return {"B": B, "value": round(B * steps / elapsed, 3), "unit": "calls/s",
             "ms_per_step": round(1e3 * elapsed / steps, 4),
             "note": "one fwd+bwd of the batched entry point = B graphs; every CG launch "
                     "timed by events carried in its dispatch packet",
-            "roofline": {"kernel": "cg_kernel", "bound": bound, "achieved": round(achieved, 3),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "work_per_launch": B * work, "avg_launch_us": round(avg_s * 1e6, 3),
-                         "launches": cnt,
-                         "traffic": pmc_traffic(f"{c['name']}_b{B}", "cg_kernel"),
-                         "rocprof_stats": _newest_profile(f"*_{c['name']}_b{B}_kernel_stats.csv")},
+            "roofline": roof,
             "gram_mfma_pmc": gram_mfma_pmc(f"{c['name']}_b{B}")}
 
 
@@ -472,22 +504,33 @@ def main():
         nnz_uu = int(np.sum((rows >= c["base"]) & (col >= c["base"])))
         GLL.check_status()
         iters = _cg_iters(X, Y, tau, eps, k, gbar)
-        units = kernel_units(c, (int(rp[-1]), nnz_uu), iters[0], iters[1], isinstance(eps, str))
+        gstats = (int(rp[-1]), nnz_uu)
+        units = kernel_units(c, gstats, iters[0], iters[1], isinstance(eps, str))
+        cg_iter_work = cg_iteration_bytes(c, gstats, iters[0], iters[1])
         bound, work = units[dominant]
         avg_s = ms / cnt / 1e3
         if bound == "mfma":
             achieved, peak, unit = work / avg_s / 1e12, GRAM_ROOF_TFS, "TFLOP/s"
         else:
             achieved, peak, unit = work / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
+        traffic = pmc_traffic(a.config, dominant)
         roofline = {"kernel": dominant, "bound": bound, "achieved": round(achieved, 3),
                     "peak": peak, "unit": unit, "frac": round(achieved / peak, 5),
-                    "traffic": pmc_traffic(a.config, dominant), "work_per_launch": work,
+                    "traffic": traffic, "work_per_launch": work,
                     "avg_launch_us": round(avg_s * 1e6, 3), "launches": cnt,
                     "cg_iters_fwd_bwd": list(iters),
                     "gram_mfma_pmc": gram_mfma_pmc(a.config)}
-        # whole-call roofline: kNN at its MFMA roof + every other byte at HBM
+        if dominant == "cg_kernel":
+            roofline["definition"] = ("SURVEY §8d SpMV roofline: B_spmv x iterations / CG launch "
+                                      "time / 8 TB/s, B_spmv = 8 nnz_off(Luu) + 8 m + 8 m C")
+            roofline["spmv_frac"] = roofline["frac"]
+            roofline.update(cg_roofline_extras(work, cg_iter_work, avg_s, traffic))
+        # whole-call roofline: kNN at its MFMA roof + every other byte at HBM,
+        # a CG priced per whole iteration (B_spmv + 28 mC)
         f_knn = units["gram_d2_kernel"][1]
-        b_rest = sum(w_ * per_kernel[kn]["launches_per_step"] for kn, (b_, w_) in units.items()
+        call_units = dict(units)
+        call_units["cg_kernel"] = ("hbm", cg_iter_work)
+        b_rest = sum(w_ * per_kernel[kn]["launches_per_step"] for kn, (b_, w_) in call_units.items()
                      if b_ == "hbm" and kn in per_kernel)
         call_roof_s = {  # SURVEY §8d prices the kNN at the fp32 MFMA peak; the split-bf16 roof
                          # is what the Gram here actually runs on (both reported, labelled)
@@ -503,7 +546,7 @@ def main():
 
     batched = None
     if a.batch > 0 and roofline is not None:
-        batched = batched_measure(c, eps, tau, k, a.batch, units, dev, rank)
+        batched = batched_measure(c, eps, tau, k, a.batch, units, cg_iter_work, dev, rank)
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:

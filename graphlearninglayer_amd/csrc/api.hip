@@ -248,13 +248,15 @@ int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const f
                const float* b, float* x, float atol, int max_iter, int32_t* iters,
                int32_t* nonconv, void* workspace, void* stream) {
     if (m < 1 || C < 1 || !row_ptr || !col || !val || !b || !x) return GLL_ERR_INVALID_ARG;
-    if (m > 2048 && C <= 16) {   // whole-GPU cooperative CG (lanes per row from nnz ~ 8 m)
+    if (m > 2048 && C <= 16) {   // whole-GPU CG (nnz unknown here: the whole LDS slice)
         if (!workspace) return GLL_ERR_INVALID_ARG;
-        const hipError_t e = launch_cg_grid_csr(m, C, row_ptr, col, val, int64_t(m) * 8, b, x,
+        prof_begin(GLL_K_CG, static_cast<hipStream_t>(stream));
+        const hipError_t e = launch_cg_grid_csr(m, C, row_ptr, col, val, -1, b, x,
                                                 atol, max_iter > 0 ? max_iter : 100000, iters,
                                                 nonconv, nullptr,
                                                 static_cast<float*>(workspace),
                                                 static_cast<hipStream_t>(stream));
+        prof_end(GLL_K_CG, static_cast<hipStream_t>(stream));
         if (e != hipErrorNotSupported) return hip_status(e);
         // past the grid kernel's capacity: per-column CG with the vectors in the workspace
     }

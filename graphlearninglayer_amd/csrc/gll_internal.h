@@ -458,6 +458,10 @@ __device__ __forceinline__ T* gshift_br_at(T* p, size_t stride, int g) {
 // Launch-error report (GLL_DEBUG=1 in the environment): which launcher failed and why.
 hipError_t launch_status(const char* what);
 
+// Opt a kernel into all of the 160 KiB of LDS its static allocation leaves for dynamic use
+// (once per kernel; solve.hip).
+void allow_full_lds(const void* fn);
+
 // Every kernel goes out through launch_k.  When prof_begin has armed an event pair for the next
 // launch (gll_prof_enable: bench.py times its dominant kernel inside the timed region), the
 // events ride in the dispatch packet itself (hipExtLaunchKernelGGL start / stop), so they time

@@ -1,20 +1,27 @@
 // gridcg.hip -- Jacobi-preconditioned CG over the whole GPU, for systems too large for one
 // workgroup per right-hand side (the Luu solves of big graphs -- stress, utils.laplace at
-// n ~ 60k -- and gll_cg_csr).  Same algorithm as the per-column kernels of solve.hip and as
+// n ~ 60k -- and gll_cg_csr).  Same iteration as the per-column kernels of solve.hip and as
 // stable_conjgrad (/root/reference/GLL.py:247-276, without its p-aliasing quirk): every
 // column runs its own PCG with per-column step sizes, and a column is frozen once it meets
 // its tolerance (GLL.py:258-268 masks alpha/beta the same way).
 //
-// One cooperative launch of persistent workgroups (G <= the co-resident capacity the runtime
-// checks: the launch is refused, not queued, when the grid cannot be resident at once), grid
-// barriers between phases:
-//   A  q = A p  (LPR lanes per row, all C columns per gathered entry), partial (p, q)
-//   B  x += a p, r -= a q, z = M r, partial (r, r), (r, z)
-//   C  p = z + b p
+// cg_gv_kernel (round 3, the default): pipelined PCG (Ghysels & Vanroose 2014, Alg. 4) --
+// ONE grid barrier per iteration.  Before the barrier a workgroup publishes m = M w for its
+// rows together with its partial dot products (r,u), (w,u), (r,r); after it, the SpMV
+// n = A m gathers the published m while the partials are summed, and every vector update is
+// local.  The workgroup's slice of the matrix (column byte offsets and values) is staged in
+// LDS once per solve, so an iteration reads nothing from global memory but the one published
+// vector and the partials.  Rows past the LDS capacity read their entries from the CSR.
+//
+// cg_grid_classic_kernel (round 1-2; GLL_GRID_CLASSIC=1 for A/B): classic two-reduction PCG,
+// two grid barriers per iteration, matrix entries and two vectors (z, p) gathered from global
+// memory every iteration.
+//
 // Dot products: each workgroup writes its partial sums, and after the barrier EVERY
 // workgroup adds all partials in the same fixed order -- so every workgroup derives
 // bitwise identical step sizes and convergence decisions (no broadcast, deterministic).
-// Vectors are m x C row-major fp32 in the workspace (a gathered row is C contiguous floats).
+// Published vectors are m x Cp row-major fp32 in the workspace (a gathered row is Cp
+// contiguous floats, Cp = C rounded up to 4).
 #include <algorithm>
 #include <cstdio>
 
@@ -189,7 +196,7 @@ __device__ __forceinline__ f32x4 quad_of(const float* s, int q) {
 // (two 16-B sc1 loads per quad) and xor-reduce; phase B updates the owned quads.  Two grid
 // barriers per iteration; only the published p / z rows and the partials cross workgroups.
 template <class Mat, int LPR, int RPG>
-__global__ __launch_bounds__(kGT) void cg_grid_kernel(Mat A, GridCgArgs a) {
+__global__ __launch_bounds__(kGT) void cg_grid_classic_kernel(Mat A, GridCgArgs a) {
     GLL_TRACE_SCOPE(0);
     __shared__ float red[256];
     __shared__ float s_rz[kGCM], s_tol2[kGCM], s_alpha[kGCM], s_beta[kGCM], s_tot[3 * kGCM];
@@ -416,9 +423,455 @@ __global__ __launch_bounds__(kGT) void cg_grid_kernel(Mat A, GridCgArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Pipelined whole-GPU PCG (cg_gv_kernel)
+// ---------------------------------------------------------------------------------------
+constexpr int kMaxG = 256;            // workgroups of one pipelined solve (<= one per CU)
+constexpr int kGvMaxRows = 512;       // rows per workgroup: NG x RPG <= 64 x 8
+constexpr int kSyncLine = 32;         // words per sync counter (one 128-B line each)
+constexpr int kSyncWords = 10 * kSyncLine;   // 8 group counters, the top counter, failure word
+
+struct GvArgs {
+    int m, C, Cp, NQ, PW, max_iter;   // PW: partial floats per workgroup (32 or 64)
+    float rtol, atol;                 // per column: stop when ||r_c|| <= max(atol, rtol ||b_c||)
+    const void* b;                    // m x C right-hand sides, b_dtype
+    int b_dtype;
+    double* out64;                    // m x C results (optional)
+    float* out32;                     // m x C results (optional)
+    float* V;                         // [2][m][Cp] published vectors (u0, then m_i), by parity
+    float* part;                      // [2][kMaxG][PW] partial sums, by parity
+    unsigned* sync;                   // kSyncWords, zeroed before the launch
+    int rows_per_wg;
+    int lds_cap;                      // matrix entries the dynamic LDS slice holds
+    int hier;                         // two-level barrier (8 counters, then one)
+    int diag_fail;                    // GLL_FLAG_DIAG_GRID_FAIL (tests only)
+    int32_t* st_iters;
+    int32_t* st_nonconv;
+    int32_t* st_failed;
+};
+
+// Grid barrier of the pipelined kernel.  Every wave drains its sc1 stores (asm vmcnt(0):
+// MI355X_MICROARCH.md's compiler hazard), the workgroup meets, and lane 0 arrives:
+//  - flat: a relaxed agent-scope add to the top counter (G arrivals per epoch);
+//  - hier: an add to counter (block % 8) whose returned value tells the group's last
+//    arriver, which alone adds to the top counter (8 arrivals per epoch).
+// Placement-independent either way (the groups are block-index classes, not XCDs; they only
+// coincide with XCDs for speed).  Lane 0 then polls the top counter with sc1 loads and
+// s_sleep; the spin is bounded and a timeout raises the failure word everyone else also
+// watches.  Monotonic counters: epoch e waits for e x arrivals.
+__device__ __forceinline__ bool gv_barrier(unsigned* sync, unsigned epoch, int G, int hier,
+                                           int* s_ok) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned* top = sync + 8 * kSyncLine;
+        unsigned* fail = sync + 9 * kSyncLine;
+        unsigned target;
+        if (hier) {
+            const int ng = G < 8 ? G : 8;
+            const int g = int(blockIdx.x) % ng;
+            const unsigned gs = unsigned((G - g + ng - 1) / ng);
+            const unsigned old = __hip_atomic_fetch_add(sync + g * kSyncLine, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            if (old + 1u == epoch * gs)
+                __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            target = epoch * unsigned(ng);
+        } else {
+            __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            target = epoch * unsigned(G);
+        }
+        int ok = 1;
+        unsigned spins = 0;
+        while (__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if ((++spins & 1023u) == 0) {
+                if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    ok = 0;
+                    break;
+                }
+                if (spins > (1u << 24)) {   // ~1 s: a workgroup never arrived
+                    __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = 0;
+                    break;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler order only
+        *s_ok = ok;
+    }
+    __syncthreads();
+    return *s_ok != 0;
+}
+
+// Sum over each aligned group of LPR lanes, result in every lane of the group (DPP: quad
+// butterflies, then the half-row and row mirrors).  Fixed order -> deterministic.
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+    v = dpp_add<0xB1, 0xf>(v);                       // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E, 0xf>(v);                       // quad_perm [2,3,0,1]
+    if constexpr (LPR >= 8) v = dpp_add<0x141, 0xf>(v);   // row_half_mirror
+    if constexpr (LPR >= 16) v = dpp_add<0x140, 0xf>(v);  // row_mirror
+    return v;
+}
+
+__device__ __forceinline__ int wave_excl_scan(int v, int* total) {
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const int y = __shfl_up(x, off);
+        if (lane_id() >= off) x += y;
+    }
+    *total = __shfl(x, kWave - 1);
+    return x - v;
+}
+
+constexpr int kOob = 0x7FFFFFF0;   // buffer offset past any num_records: the load returns 0
+
+// Workgroup w owns rows [w R, (w+1) R).  A group of LPR lanes owns up to RPG of them (local
+// rows grp, grp + NG, ...); lane li of the group owns column quad li (columns 4li..4li+3) of
+// those rows and keeps x, r, u, w, p, s, q, z for them in registers for the whole solve.
+// The group's lanes split each row's entries for the gathers and sum them by DPP.
+template <class Mat, int NT, int LPR, int RPG>
+__global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
+    GLL_TRACE_SCOPE(1);
+    extern __shared__ __attribute__((aligned(16))) int2 s_ent[];   // (byte offset, value bits)
+    __shared__ int s_len[kGvMaxRows];
+    __shared__ float s_wp[NT / kWave][64];        // per-wave partials, slots [0,3C)
+    __shared__ f32x4 s_red[NT / kWave][16];       // per-wave sums of the loaded partials
+    __shared__ float s_tot[64];
+    __shared__ float s_alpha[kGCM], s_beta[kGCM], s_gold[kGCM], s_aold[kGCM], s_tol2[kGCM];
+    __shared__ int s_act[kGCM];
+    __shared__ int s_any, s_ok;
+    constexpr int NG = NT / LPR;
+    constexpr int NW = NT / kWave;
+    constexpr int JP = kMaxG * 16 / NT;   // partial float4 loads per thread
+    const int m = a.m, C = a.C, Cp = a.Cp, NQ = a.NQ, PW = a.PW;
+    const int G = gridDim.x;
+    const int r0 = blockIdx.x * a.rows_per_wg;
+    const int r1 = min(m, r0 + a.rows_per_wg);
+    const int li = threadIdx.x % LPR;
+    const int grp = threadIdx.x / LPR;
+    const int wv = threadIdx.x >> 6, lane = lane_id();
+    const bool qown = li < NQ;
+    const int rowB = Cp * 4;
+    const int vbytes = m * rowB;
+    const __amdgpu_buffer_rsrc_t rv0 = __builtin_amdgcn_make_buffer_rsrc(a.V, 0, vbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv1 =
+        __builtin_amdgcn_make_buffer_rsrc(a.V + size_t(m) * Cp, 0, vbytes, 0x00020000);
+    const int pbytes = G * PW * 4;
+    const __amdgpu_buffer_rsrc_t rpt0 = __builtin_amdgcn_make_buffer_rsrc(a.part, 0, pbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rpt1 =
+        __builtin_amdgcn_make_buffer_rsrc(a.part + size_t(kMaxG) * PW, 0, pbytes, 0x00020000);
+
+    // ---- the workgroup's matrix slice -> LDS (once per solve)
+    int len[RPG], off[RPG], gb[RPG];
+#pragma unroll
+    for (int k = 0; k < RPG; ++k) {
+        const int lr = grp + k * NG;
+        const int u = r0 + lr;
+        len[k] = 0;
+        gb[k] = 0;
+        if (u < r1) {
+            gb[k] = A.begin(u);
+            len[k] = A.end(u) - gb[k];
+        }
+        if (li == 0) s_len[lr] = len[k];
+    }
+    for (int t = threadIdx.x; t < 64; t += NT)
+        for (int w = 0; w < NW; ++w) s_wp[w][t] = 0.f;
+    __syncthreads();
+    if (threadIdx.x < kWave) {   // exclusive scan of the row lengths (wave 0)
+        int carry = 0;
+        for (int c0 = 0; c0 < NG * RPG; c0 += kWave) {
+            const int v = s_len[c0 + lane];
+            int tot;
+            const int ex = wave_excl_scan(v, &tot);
+            s_len[c0 + lane] = carry + ex;
+            carry += tot;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RPG; ++k) {
+        off[k] = s_len[grp + k * NG];
+        for (int e = li; e < len[k]; e += LPR) {
+            const int slot = off[k] + e;
+            if (slot < a.lds_cap)
+                s_ent[slot] = int2{A.column(gb[k] + e) * rowB,
+                                   __builtin_bit_cast(int, A.value(gb[k] + e))};
+        }
+    }
+
+    // n = A v over the owned rows: lane li gathers entries li, li + LPR, ... (chunks of CH per
+    // lane, every gather of a chunk in flight together), the group sums by DPP, lane li keeps
+    // quad li.  Dead entries load from an out-of-range offset (the buffer returns 0).
+    constexpr int CH = NT >= 1024 ? 2 : 4;   // 16 waves: fewer gathers per lane, no spills
+    auto spmv = [&](int k, __amdgpu_buffer_rsrc_t rv) -> f32x4 {
+        f32x4 acc[kGCM / 4];
+#pragma unroll
+        for (int qq = 0; qq < kGCM / 4; ++qq) acc[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int eb = li; eb < len[k]; eb += CH * LPR) {
+            int co[CH];
+            float vv[CH];
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const int e = eb + t * LPR;
+                int2 en = int2{kOob, 0};
+                if (e < len[k]) {
+                    const int slot = off[k] + e;
+                    en = slot < a.lds_cap ? s_ent[slot]
+                                          : int2{A.column(gb[k] + e) * rowB,
+                                                 __builtin_bit_cast(int, A.value(gb[k] + e))};
+                }
+                co[t] = en.x;
+                vv[t] = __builtin_bit_cast(float, en.y);
+            }
+#pragma unroll
+            for (int qq = 0; qq < kGCM / 4; ++qq) {
+                if (qq < NQ) {
+                    f32x4 g[CH];
+#pragma unroll
+                    for (int t = 0; t < CH; ++t)
+                        g[t] = __builtin_amdgcn_raw_buffer_load_b128(rv, co[t] + 16 * qq, 0, kSc1);
+#pragma unroll
+                    for (int t = 0; t < CH; ++t) acc[qq] += vv[t] * g[t];
+                }
+            }
+        }
+        f32x4 mine = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int qq = 0; qq < kGCM / 4; ++qq) {
+            if (qq < NQ) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) acc[qq][t] = group_sum<LPR>(acc[qq][t]);
+                mine = li == qq ? acc[qq] : mine;
+            }
+        }
+        return mine;
+    };
+
+    // ---- setup: x = 0, r = b (decoupled rows: 0), u = M r published for w = A u
+    f32x4 x[RPG], r[RPG], u[RPG], w[RPG], p[RPG], s[RPG], q[RPG], z[RPG];
+    float mi[RPG], dg[RPG];
+#pragma unroll
+    for (int k = 0; k < RPG; ++k) {
+        const int uu = r0 + grp + k * NG;
+        x[k] = r[k] = u[k] = w[k] = p[k] = s[k] = q[k] = z[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        mi[k] = dg[k] = 0.f;
+        if (uu < r1) {
+            dg[k] = A.diagonal(uu);
+            mi[k] = dg[k] > 0.f ? 1.f / dg[k] : 0.f;
+            if (qown) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int c = 4 * li + t;
+                    const float bu = c < C ? rhs_at(a.b, a.b_dtype, size_t(uu) * C + c) : 0.f;
+                    r[k][t] = mi[k] > 0.f ? bu : 0.f;
+                }
+                u[k] = mi[k] * r[k];
+                __builtin_amdgcn_raw_buffer_store_b128(u[k], rv0, uu * rowB + 16 * li, 0, kSc1);
+            }
+        }
+    }
+    if (threadIdx.x < kGCM) {
+        s_act[threadIdx.x] = threadIdx.x < C ? 1 : 0;
+        s_alpha[threadIdx.x] = s_beta[threadIdx.x] = 0.f;
+        s_gold[threadIdx.x] = s_aold[threadIdx.x] = 1.f;
+        s_tol2[threadIdx.x] = 0.f;
+    }
+    unsigned epoch = 0;
+    bool ok = gv_barrier(a.sync, ++epoch, G, a.hier, &s_ok);
+#pragma unroll
+    for (int k = 0; k < RPG; ++k) {
+        const int uu = r0 + grp + k * NG;
+        if (uu < r1) {
+            const f32x4 o = spmv(k, rv0);
+            w[k] = Mat::kSeparateDiag ? dg[k] * u[k] + o : o;
+        }
+    }
+
+    int it = 0;
+    GLL_TRACE_PT(8);
+    while (ok) {
+        const int pub = (it + 1) & 1;
+        const __amdgpu_buffer_rsrc_t rvp = pub ? rv1 : rv0;
+        const __amdgpu_buffer_rsrc_t rpp = pub ? rpt1 : rpt0;
+        // ---- local: partial (r,u), (w,u), (r,r); publish m = M w
+        {
+            f32x4 pg = {0.f, 0.f, 0.f, 0.f}, pd = pg, pr = pg;
+#pragma unroll
+            for (int k = 0; k < RPG; ++k) {
+                const int uu = r0 + grp + k * NG;
+                if (uu < r1 && qown) {
+                    pg += r[k] * u[k];
+                    pd += w[k] * u[k];
+                    pr += r[k] * r[k];
+                    __builtin_amdgcn_raw_buffer_store_b128(mi[k] * w[k], rvp, uu * rowB + 16 * li,
+                                                           0, kSc1);
+                }
+            }
+            // lanes of one quad across the wave's row groups, then the waves in order
+#pragma unroll
+            for (int o = LPR; o < kWave; o <<= 1) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    pg[t] += __shfl_xor(pg[t], o);
+                    pd[t] += __shfl_xor(pd[t], o);
+                    pr[t] += __shfl_xor(pr[t], o);
+                }
+            }
+            if (lane < LPR && qown) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int c = 4 * li + t;
+                    if (c < C) {
+                        s_wp[wv][c] = pg[t];
+                        s_wp[wv][C + c] = pd[t];
+                        s_wp[wv][2 * C + c] = pr[t];
+                    }
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x < PW / 4) {
+                f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int w_ = 0; w_ < NW; ++w_) v += quad_of(s_wp[w_], threadIdx.x);
+                __builtin_amdgcn_raw_buffer_store_b128(v, rpp, (blockIdx.x * PW + 4 * threadIdx.x) * 4,
+                                                       0, kSc1);
+            }
+        }
+        ok = gv_barrier(a.sync, ++epoch, G, a.hier, &s_ok);
+        if (a.diag_fail && it == 2) ok = false;   // injected failure (uniform over the grid)
+        if (!ok) break;
+        if (it == 0) GLL_TRACE_PT(9);
+        // ---- the partials of every workgroup (all loads in flight; out-of-range -> 0) ...
+        const int NQP = PW / 4;
+        f32x4 pl[JP];
+#pragma unroll
+        for (int j = 0; j < JP; ++j)
+            pl[j] = __builtin_amdgcn_raw_buffer_load_b128(rpp, (threadIdx.x + NT * j) * 16, 0, kSc1);
+        // ---- ... while n = A m gathers the published m
+        f32x4 nn[RPG];
+#pragma unroll
+        for (int k = 0; k < RPG; ++k) {
+            const int uu = r0 + grp + k * NG;
+            nn[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (uu < r1) {
+                const f32x4 o = spmv(k, rvp);
+                nn[k] = Mat::kSeparateDiag ? dg[k] * (mi[k] * w[k]) + o : o;
+            }
+        }
+        // slot q = threadIdx % NQP: fixed order over j, then lanes, then waves
+        {
+            f32x4 v = pl[0];
+#pragma unroll
+            for (int j = 1; j < JP; ++j) v += pl[j];
+            for (int o = NQP; o < kWave; o <<= 1) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) v[t] += __shfl_xor(v[t], o);
+            }
+            if (lane < NQP) s_red[wv][lane] = v;
+            __syncthreads();
+            if (threadIdx.x < NQP) {
+                f32x4 t4 = s_red[0][threadIdx.x];
+#pragma unroll
+                for (int w_ = 1; w_ < NW; ++w_) t4 += s_red[w_][threadIdx.x];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) s_tot[4 * threadIdx.x + t] = t4[t];
+            }
+            __syncthreads();
+        }
+        // ---- step sizes (one lane per column, identical in every workgroup)
+        if (threadIdx.x < kWave) {
+            const int c = threadIdx.x;
+            int act = 0;
+            if (c < C) {
+                const float gam = s_tot[c], del = s_tot[C + c], rho = s_tot[2 * C + c];
+                if (it == 0) {
+                    const float tl = fmaxf(a.atol, a.rtol * sqrtf(rho));
+                    s_tol2[c] = tl * tl;
+                }
+                act = s_act[c];
+                if (act == 1 && rho <= s_tol2[c]) act = 0;   // converged
+                float al = 0.f, be = 0.f;
+                if (act == 1) {
+                    float den = del;
+                    if (it > 0) {
+                        be = gam / s_gold[c];
+                        den = del - be * gam / s_aold[c];
+                    }
+                    if (!(den > 0.f) || !(gam > 0.f)) {
+                        act = 2;   // breakdown / NaN: stops, not converged
+                        be = 0.f;
+                    } else {
+                        al = gam / den;
+                        s_gold[c] = gam;
+                        s_aold[c] = al;
+                    }
+                }
+                s_act[c] = act;
+                s_alpha[c] = act == 1 ? al : 0.f;
+                s_beta[c] = act == 1 ? be : 0.f;
+            }
+            const unsigned long long any = __ballot(c < C && act == 1);
+            if (c == 0) s_any = (any != 0ull && it < a.max_iter) ? 1 : 0;
+        }
+        __syncthreads();
+        if (!s_any) break;
+        // ---- local updates (Ghysels-Vanroose recurrences)
+        {
+            const f32x4 al = quad_of(s_alpha, li < kGCM / 4 ? li : 0);
+            const f32x4 be = quad_of(s_beta, li < kGCM / 4 ? li : 0);
+#pragma unroll
+            for (int k = 0; k < RPG; ++k) {
+                const int uu = r0 + grp + k * NG;
+                if (uu >= r1 || !qown) continue;
+                const f32x4 mk = mi[k] * w[k];
+                z[k] = nn[k] + be * z[k];
+                q[k] = mk + be * q[k];
+                s[k] = w[k] + be * s[k];
+                p[k] = u[k] + be * p[k];
+                x[k] += al * p[k];
+                r[k] -= al * s[k];
+                u[k] -= al * q[k];
+                w[k] -= al * z[k];
+            }
+        }
+        ++it;
+    }
+    GLL_TRACE_PT(10);
+    // a failed grid barrier (a workgroup never arrived within ~1 s) leaves x partial: the
+    // outputs become NaN and GLL_ST_SOLVE_FAILED is raised (see the classic kernel)
+    const float nanf_ = __builtin_nanf("");
+#pragma unroll
+    for (int k = 0; k < RPG; ++k) {
+        const int uu = r0 + grp + k * NG;
+        if (uu >= r1 || !qown) continue;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int c = 4 * li + t;
+            if (c < C) {
+                const size_t i = size_t(uu) * C + c;
+                const float xv = ok ? x[k][t] : nanf_;
+                if (a.out64) a.out64[i] = double(xv);
+                if (a.out32) a.out32[i] = xv;
+            }
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int nonconv = 0;
+        for (int c = 0; c < C; ++c) nonconv += s_act[c] != 0 ? 1 : 0;
+        if (a.st_iters) atomicMax(a.st_iters, it);
+        if (a.st_nonconv && (nonconv || !ok)) atomicAdd(a.st_nonconv, ok ? nonconv : C);
+        if (!ok && a.st_failed) atomicOr(a.st_failed, 1);
+    }
+}
+
 size_t grid_cg_workspace_floats(int m, int C) {
     const size_t Cp = size_t((C + 3) & ~3);
-    return 64 + size_t(3) * m * Cp + size_t(3) * kGCM * 1024;
+    const size_t classic = 64 + size_t(3) * m * Cp + size_t(3) * kGCM * 1024;
+    const size_t gv = kSyncWords + size_t(2) * m * Cp + size_t(2) * kMaxG * 64;
+    return classic > gv ? classic : gv;
 }
 
 static int cu_count() {
@@ -432,14 +885,15 @@ static int cu_count() {
     return cus;
 }
 
-// Workgroups of one kernel instance that can be resident at once on the whole device.
+// Workgroups of one kernel instance that can be resident at once on the whole device (the
+// classic kernel, no dynamic LDS).
 template <class Mat, int LPR, int RPG>
 static int coresident_capacity() {
     static int cap = -1;
     if (cap < 0) {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void*>(cg_grid_kernel<Mat, LPR, RPG>), kGT, 0) !=
+                &nb, reinterpret_cast<const void*>(cg_grid_classic_kernel<Mat, LPR, RPG>), kGT, 0) !=
             hipSuccess)
             nb = 1;
         (void)hipGetLastError();
@@ -448,28 +902,61 @@ static int coresident_capacity() {
     return cap;
 }
 
-static bool coop_supported() {
+// GLL_GRID_COOP=1: start the grid with hipLaunchCooperativeKernel (diagnostic).  The default
+// is an ordinary launch sized within the co-resident capacity: MI355X_MICROARCH.md's price
+// list puts the cooperative launch at +15-19 us of host time per launch for no residency the
+// ordinary launch lacks (the runtime's check even accepts one workgroup per CU more than the
+// hardware admits at some SGPR counts), and under rocprofv3 a process that made one crashed
+// at exit.  The bounded barrier turns any residency failure into NaN outputs
+// + GLL_ST_SOLVE_FAILED instead of a hang.
+static bool coop_requested() {
     static int v = -1;
     if (v < 0) {
         int dev = 0, a = 0;
         (void)hipGetDevice(&dev);
         if (hipDeviceGetAttribute(&a, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess) a = 0;
         (void)hipGetLastError();
-        const char* env = getenv("GLL_GRID_COOP");   // diagnostic A/B: 0 = ordinary launch
-        v = (a != 0 && !(env && env[0] == '0')) ? 1 : 0;
+        const char* env = getenv("GLL_GRID_COOP");
+        v = (a != 0 && env && env[0] == '1') ? 1 : 0;
     }
     return v == 1;
 }
 
-// G workgroups of rows_per_wg rows.  Cooperative launch: the runtime guarantees that all G are
-// resident together or refuses the launch (hipErrorCooperativeLaunchTooLarge), so the grid
-// barrier cannot wait on a workgroup that was never scheduled.  (Without cooperative-launch
-// support: an ordinary launch sized within the occupancy capacity; the bounded barrier then
-// turns a co-residency failure into NaN outputs + GLL_ST_SOLVE_FAILED.)
+static int env_int(const char* name, int dflt) {   // read per call (tests set them)
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+template <typename F, typename... Args>
+static hipError_t launch_persistent(F fn, int G, int nt, size_t lds, hipStream_t s,
+                                    const char* what, Args... args) {
+    if (!coop_requested()) {
+        launch_k(fn, dim3(unsigned(G)), dim3(unsigned(nt)), lds, s, args...);
+        return launch_status(what);
+    }
+    void* argv[] = {&args...};
+    const ArmedLaunch armed = g_armed;   // bench timing: events around the launch
+    g_armed = ArmedLaunch{};
+    if (armed.kid >= 0) (void)hipEventRecord(armed.e0, s);
+    hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(unsigned(G)),
+                                              dim3(unsigned(nt)), argv, unsigned(lds), s);
+    if (armed.kid >= 0) (void)hipEventRecord(armed.e1, s);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        if (getenv("GLL_DEBUG"))
+            fprintf(stderr, "gll: %s (cooperative, G=%d): %s\n", what, G, hipGetErrorString(e));
+        return e;
+    }
+    return launch_status(what);
+}
+
+// ---- classic kernel: G workgroups of rows_per_wg rows
 template <class Mat, int LPR, int RPG>
 static hipError_t launch_grid(const Mat& A, GridCgArgs a, int G, float* ws, hipStream_t s) {
     a.rows_per_wg = (a.m + G - 1) / G;
     G = (a.m + a.rows_per_wg - 1) / a.rows_per_wg;
+    if (G > 1024 || G > coresident_capacity<Mat, LPR, RPG>())   // partials hold 1024 workgroups
+        return hipErrorCooperativeLaunchTooLarge;
     a.Cp = (a.C + 3) & ~3;
     a.sync = reinterpret_cast<unsigned*>(ws);          // 16-B block at the region's start
     a.Pbuf = ws + 64;                                   // 256-B aligned: 16-B buffer accesses
@@ -477,43 +964,16 @@ static hipError_t launch_grid(const Mat& A, GridCgArgs a, int G, float* ws, hipS
     a.part = a.Zbuf + size_t(a.m) * a.Cp;
     hipError_t e = hipMemsetAsync(a.sync, 0, 16, s);
     if (e != hipSuccess) return e;
-    auto fn = cg_grid_kernel<Mat, LPR, RPG>;
-    if (!coop_supported()) {
-        if (G > coresident_capacity<Mat, LPR, RPG>()) return hipErrorCooperativeLaunchTooLarge;
-        launch_k(fn, dim3(unsigned(G)), kGT, 0, s, A, a);
-        return launch_status("gridcg.hip:launch_grid");
-    }
-    Mat Acopy = A;
-    void* args[] = {&Acopy, &a};
-    static const bool dbg_launch = getenv("GLL_DEBUG") != nullptr;
-    if (dbg_launch)
-        fprintf(stderr, "gll: grid CG cooperative launch G=%d rows/wg=%d LPR=%d RPG=%d cap=%d\n",
-                G, a.rows_per_wg, LPR, RPG, coresident_capacity<Mat, LPR, RPG>());
-    const ArmedLaunch armed = g_armed;   // bench timing: events around the launch
-    g_armed = ArmedLaunch{};
-    if (armed.kid >= 0) (void)hipEventRecord(armed.e0, s);
-    e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(unsigned(G)),
-                                   dim3(kGT), args, 0, s);
-    if (armed.kid >= 0) (void)hipEventRecord(armed.e1, s);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        static const bool dbg = getenv("GLL_DEBUG") != nullptr;
-        if (dbg) fprintf(stderr, "gll: gridcg.hip:launch_grid (cooperative, G=%d): %s\n", G,
-                         hipGetErrorString(e));
-        return e;
-    }
-    return launch_status("gridcg.hip:launch_grid");
+    return launch_persistent(cg_grid_classic_kernel<Mat, LPR, RPG>, G, kGT, 0, s,
+                             "gridcg.hip:launch_grid", A, a);
 }
 
 // Lanes per row from the mean row length; rows per lane group (registers) and workgroups:
 // the fewest rows per group that keep the grid within 64 workgroups (barrier cost grows with
-// the arrivals), else within the co-resident capacity.  Returns hipErrorNotSupported when no
-// configuration holds the system (rows past capacity x 32 x 8): the caller then runs the
-// per-column kernels with the Krylov vectors in the workspace, which take any size.
-// `oversub` (GLL_FLAG_DIAG_GRID_OVERSUB, tests only) asks for twice the capacity.
+// the arrivals), else within the co-resident capacity (at most 1024, the partials buffer).
 template <class Mat>
-static hipError_t dispatch_grid(const Mat& A, const GridCgArgs& a, int64_t nnz, float* ws,
-                                bool oversub, hipStream_t s) {
+static hipError_t dispatch_classic(const Mat& A, const GridCgArgs& a, int64_t nnz, float* ws,
+                                   bool oversub, hipStream_t s) {
     const int64_t avg = a.m > 0 ? nnz / a.m : 0;
     const int LPR = avg <= 12 ? 4 : 8;
     const int64_t NG = kGT / LPR;
@@ -521,9 +981,8 @@ static hipError_t dispatch_grid(const Mat& A, const GridCgArgs& a, int64_t nnz, 
                                             coresident_capacity<Mat, 4, 8>())
                                  : std::min(coresident_capacity<Mat, 8, 1>(),
                                             coresident_capacity<Mat, 8, 8>());
-    const char* cap_env = getenv("GLL_GRID_CAP");   // tests: shrink the capacity (read per call)
-    const int64_t cap_lim = cap_env ? std::max(1, atoi(cap_env)) : cap;
-    cap = std::min(cap, cap_lim);
+    cap = std::min<int64_t>(cap, 1024);
+    cap = std::min<int64_t>(cap, std::max(1, env_int("GLL_GRID_CAP", int(cap))));
     int rpg = 0;
     int64_t G = 0;
     for (int64_t lim : {std::min<int64_t>(64, cap), cap}) {
@@ -539,8 +998,6 @@ static hipError_t dispatch_grid(const Mat& A, const GridCgArgs& a, int64_t nnz, 
     }
     if (!rpg) return hipErrorNotSupported;
     if (oversub) {
-        // one row per workgroup: far past what the hardware can hold at once (at most 8
-        // workgroups of kGT threads per CU), whatever the occupancy query under-reports
         rpg = 1;
         G = std::min<int64_t>(a.m, int64_t(1) << 20);
     }
@@ -551,6 +1008,106 @@ static hipError_t dispatch_grid(const Mat& A, const GridCgArgs& a, int64_t nnz, 
     GLL_GRID(8, 1); GLL_GRID(8, 2); GLL_GRID(8, 4); GLL_GRID(8, 8);
 #undef GLL_GRID
     return hipErrorInvalidValue;
+}
+
+// ---- pipelined kernel
+template <class Mat, int NT, int LPR, int RPG>
+static hipError_t launch_gv(const Mat& A, GvArgs a, int G, int64_t nnz, float* ws, hipStream_t s) {
+    a.rows_per_wg = (a.m + G - 1) / G;
+    G = (a.m + a.rows_per_wg - 1) / a.rows_per_wg;
+    auto fn = cg_gv_kernel<Mat, NT, LPR, RPG>;
+    allow_full_lds(reinterpret_cast<const void*>(fn));
+    // the slice: the workgroup's share of the entries with a quarter of margin (rows beyond it
+    // read the CSR), within what the static LDS leaves; unknown nnz (< 0): all of it
+    hipFuncAttributes at{};
+    size_t stat = 8192;
+    if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(fn)) == hipSuccess)
+        stat = at.sharedSizeBytes;
+    (void)hipGetLastError();
+    const size_t lds_max = (size_t(160) * 1024 - stat - 256) & ~size_t(15);
+    size_t lds = lds_max;
+    if (nnz >= 0) {
+        const int64_t per = (nnz + G - 1) / G;
+        lds = std::min(lds_max, size_t(per + per / 4 + 64) * 8);
+    }
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(fn), NT,
+                                                     lds) != hipSuccess)
+        nb = 0;
+    (void)hipGetLastError();
+    if (nb < 1 || G > kMaxG || G > cu_count()) return hipErrorCooperativeLaunchTooLarge;
+    a.sync = reinterpret_cast<unsigned*>(ws);
+    a.V = ws + kSyncWords;                       // 1280 B in: 256-B aligned
+    a.part = a.V + size_t(2) * a.m * a.Cp;
+    a.lds_cap = int(lds / 8);
+    hipError_t e = hipMemsetAsync(a.sync, 0, kSyncWords * sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
+    static const bool dbg = getenv("GLL_DEBUG") != nullptr;
+    if (dbg)
+        fprintf(stderr, "gll: grid CG (pipelined) G=%d rows/wg=%d NT=%d LPR=%d RPG=%d lds=%zu "
+                "hier=%d\n", G, a.rows_per_wg, NT, LPR, RPG, lds, a.hier);
+    return launch_persistent(fn, G, NT, lds, s, "gridcg.hip:launch_gv", A, a);
+}
+
+// Workgroups: one per CU at most, about 16 rows each (GLL_GRID_G overrides, diagnostic);
+// lanes per row as wide as the rows per workgroup allow; up to 512 rows per workgroup (m <=
+// 131,072 at 256 workgroups).  hipErrorNotSupported: no configuration holds it.
+template <class Mat>
+static hipError_t dispatch_gv(const Mat& A, const GridCgArgs& c, int64_t nnz, float* ws,
+                              hipStream_t s) {
+    GvArgs a{};
+    a.m = c.m;
+    a.C = c.C;
+    a.Cp = (c.C + 3) & ~3;
+    a.NQ = (c.C + 3) >> 2;
+    a.PW = 3 * c.C <= 32 ? 32 : 64;
+    a.max_iter = c.max_iter;
+    a.rtol = c.rtol;
+    a.atol = c.atol;
+    a.b = c.b;
+    a.b_dtype = c.b_dtype;
+    a.out64 = c.out64;
+    a.out32 = c.out32;
+    a.diag_fail = c.diag_fail;
+    a.st_iters = c.st_iters;
+    a.st_nonconv = c.st_nonconv;
+    a.st_failed = c.st_failed;
+    a.hier = env_int("GLL_GRID_HIER", 1) != 0 ? 1 : 0;
+    int cap = std::min(kMaxG, cu_count());
+    cap = std::min(cap, std::max(1, env_int("GLL_GRID_CAP", cap)));
+    int G = int(std::min<int64_t>(cap, (int64_t(a.m) + 15) / 16));
+    const int Gf = env_int("GLL_GRID_G", 0);
+    if (Gf > 0) G = std::min(cap, Gf);
+    if (G < 1) G = 1;
+    const int R = (a.m + G - 1) / G;
+    // 256 threads while lanes per row can stay >= 4 with one row per lane group; 1024 threads
+    // (16 waves: more gathers in flight per CU) for long row blocks (GLL_GRID_NT overrides)
+    const int nt = env_int("GLL_GRID_NT", R <= 64 ? 256 : 1024);
+    if (nt == 256) {
+        if (R <= 16) return launch_gv<Mat, 256, 16, 1>(A, a, G, nnz, ws, s);
+        if (R <= 32) return launch_gv<Mat, 256, 8, 1>(A, a, G, nnz, ws, s);
+        if (R <= 64) return launch_gv<Mat, 256, 4, 1>(A, a, G, nnz, ws, s);
+        if (R <= 128) return launch_gv<Mat, 256, 4, 2>(A, a, G, nnz, ws, s);
+        if (R <= 256) return launch_gv<Mat, 256, 4, 4>(A, a, G, nnz, ws, s);
+    } else {
+        if (R <= 64) return launch_gv<Mat, 1024, 16, 1>(A, a, G, nnz, ws, s);
+        if (R <= 128) return launch_gv<Mat, 1024, 8, 1>(A, a, G, nnz, ws, s);
+        if (R <= 256) return launch_gv<Mat, 1024, 4, 1>(A, a, G, nnz, ws, s);
+        if (R <= 512) return launch_gv<Mat, 1024, 4, 2>(A, a, G, nnz, ws, s);
+    }
+    return hipErrorNotSupported;
+}
+
+// The pipelined kernel unless GLL_GRID_CLASSIC=1 (A/B) or the oversubscription test asks for
+// the classic sizing; past the pipelined kernel's row capacity, the classic kernel.
+template <class Mat>
+static hipError_t dispatch_grid(const Mat& A, const GridCgArgs& a, int64_t nnz, float* ws,
+                                bool oversub, hipStream_t s) {
+    if (!oversub && env_int("GLL_GRID_CLASSIC", 0) == 0) {
+        const hipError_t e = dispatch_gv(A, a, nnz, ws, s);
+        if (e != hipErrorNotSupported) return e;
+    }
+    return dispatch_classic(A, a, nnz < 0 ? int64_t(a.m) * 8 : nnz, ws, oversub, s);
 }
 
 hipError_t launch_cg_grid_luu(const Layout& L, void* wsp, const void* b, int b_dtype,
@@ -575,8 +1132,8 @@ hipError_t launch_cg_grid_luu(const Layout& L, void* wsp, const void* b, int b_d
     a.st_nonconv = st_nonconv;
     a.st_failed = st_failed;
     a.diag_fail = (L.flags & GLL_FLAG_DIAG_GRID_FAIL) ? 1 : 0;
-    // U-block entries per row ~ 1.5 (K-1) on kNN graphs (mean row length of the union)
-    const int64_t nnz_est = int64_t(L.m) * (L.K - 1) * 3 / 2;
+    // U-block entries per row ~ 1.5 (K-1) m / n on kNN graphs (union rows, U share)
+    const int64_t nnz_est = int64_t(double(L.m) * (L.K - 1) * 1.5 * double(L.m) / double(L.n)) + L.m;
     return dispatch_grid(A, a, nnz_est, L.at<float>(wsp, L.cgv),
                          (L.flags & GLL_FLAG_DIAG_GRID_OVERSUB) != 0, s);
 }

@@ -39,7 +39,7 @@ static constexpr size_t kLdsDyn = kLdsLimit - 1024;   // dynamic share, room for
 // Opt a kernel into all of the 160 KiB of LDS its static allocation leaves for dynamic use,
 // once per kernel (host-side cost).  The attribute call's status is consumed here: a failure
 // must not linger as the thread's last error and surface at an unrelated launch.
-static void allow_full_lds(const void* fn) {
+void allow_full_lds(const void* fn) {
     static std::mutex mu;
     static std::unordered_set<const void*> done;
     std::lock_guard<std::mutex> lk(mu);

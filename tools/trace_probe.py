@@ -34,26 +34,27 @@ c = CONFIGS[cfg_name]
 n, base, d, k = c["base"] + c["batch"], c["base"], c["d"], c["k"]
 eps = float(os.environ.get("TRACE_EPS", "1.0"))
 dev = torch.device("cuda", 0)
+B = int(os.environ.get("TRACE_B", "1"))   # > 1: the batched entry points, B copies of the graph
 X_np, lab = synth(base, n - base, d, r=c["r"], seed=0)
-X = torch.from_numpy(X_np).to(dev)
-Y = torch.from_numpy(one_hot(lab[:base])).to(dev)
-g = torch.from_numpy(seeded_gbar(n - base, 10)).to(dev)
+X = torch.from_numpy(np.stack([X_np] * B)).to(dev)
+Y = torch.from_numpy(np.stack([one_hot(lab[:base])] * B)).to(dev)
+g = torch.from_numpy(np.stack([seeded_gbar(n - base, 10)] * B)).to(dev)
 prob = GLL.make_problem(n, d, base, 10, k, 0.07, eps, flags=int(os.environ.get("TRACE_FLAGS", "0")))
-ws = torch.empty(lib.gll_workspace_bytes(ct.byref(prob)), dtype=torch.uint8, device=dev)
-U = torch.empty(n - base, 10, dtype=torch.float64, device=dev)
-gx = torch.empty(n, d, dtype=torch.float32, device=dev)
+ws = torch.empty(lib.gll_workspace_bytes(ct.byref(prob)) * B, dtype=torch.uint8, device=dev)
+U = torch.empty(B, n - base, 10, dtype=torch.float64, device=dev)
+gx = torch.empty(B, n, d, dtype=torch.float32, device=dev)
 s = ct.c_void_p(torch.cuda.current_stream().cuda_stream)
+vp = ct.c_void_p
 
 
 def fwd():
-    assert lib.gll_forward(ct.byref(prob), ct.c_void_p(X.data_ptr()), ct.c_void_p(Y.data_ptr()), 0,
-                           ct.c_void_p(ws.data_ptr()), ct.c_void_p(U.data_ptr()), s) == 0
+    assert lib.gll_forward_batched(ct.byref(prob), B, vp(X.data_ptr()), vp(Y.data_ptr()), 0,
+                                   vp(ws.data_ptr()), vp(U.data_ptr()), s) == 0
 
 
 def bwd():
-    assert lib.gll_backward(ct.byref(prob), ct.c_void_p(X.data_ptr()), ct.c_void_p(Y.data_ptr()), 0,
-                            ct.c_void_p(ws.data_ptr()), ct.c_void_p(g.data_ptr()), 1,
-                            ct.c_void_p(gx.data_ptr()), s) == 0
+    assert lib.gll_backward_batched(ct.byref(prob), B, vp(X.data_ptr()), vp(ws.data_ptr()),
+                                    vp(g.data_ptr()), 1, vp(gx.data_ptr()), s) == 0
 
 
 def read_all():
