@@ -32,6 +32,16 @@ import torch
 from . import _lib
 
 DEFAULT_K = 25          # GLL.py:27
+MAX_K = 57              # include/gll.h: 2 <= K <= 57 (neighbours incl. self; kMaxKm1 = 56)
+
+
+def _check_k(k, n):
+    """The kNN count the C ABI supports (include/gll.h gll_problem.K): a clear error here
+    instead of the ABI's generic 'unsupported problem size'."""
+    kk = min(int(k), int(n))
+    if kk < 2 or kk > MAX_K:
+        raise ValueError(f"k = {k} (n = {n}): the kNN count incl. self must satisfy "
+                         f"2 <= min(k, n) <= {MAX_K}")
 DEFAULT_RTOL = 1e-6     # SURVEY.md §8c: fp32 Jacobi-CG at 1e-6 matches SuperLU to <1e-5
 DEFAULT_MAX_ITER = 1000
 
@@ -191,6 +201,7 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
 
     @classmethod
     def apply(cls, X, label_matrix, tau=0, epsilon="auto", k=DEFAULT_K):
+        _check_k(k, X.shape[-2])
         ext = _ext()
         if ext is None or _grad_diag is not None:
             return super().apply(X, label_matrix, tau, epsilon, k)
@@ -285,6 +296,7 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
 def device_graph(X: torch.Tensor, k: int = DEFAULT_K, epsilon="auto"):
     """Build the symmetric kNN graph on the GPU; returns a dict of device tensors
     (knn_idx, knn_d2, eps, row_ptr, col, w, d2, deg)."""
+    _check_k(k, X.shape[0])
     dev = _device_for(X)
     n, d = X.shape
     with torch.cuda.device(dev):

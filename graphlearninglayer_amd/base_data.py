@@ -75,6 +75,7 @@ class DeviceBaseLoader:
             raise TypeError("labels must be integer class indices")
         self.data = data.to(self.device).contiguous()
         self.labels = labels.to(self.device, torch.int64).contiguous()
+        self._last_labels = None   # labels of the latest draw, in that draw's order
 
     def __len__(self) -> int:
         return int(self.data.shape[0])
@@ -82,15 +83,24 @@ class DeviceBaseLoader:
     def sample(self):
         """One draw: (images, labels) of the whole base set in a fresh random order."""
         if not self.shuffle:
+            self._last_labels = self.labels
             return self.data, self.labels
         perm = torch.randperm(len(self), device=self.device, generator=self._gen)
-        return self.data.index_select(0, perm), self.labels.index_select(0, perm)
+        lab = self.labels.index_select(0, perm)
+        self._last_labels = lab
+        return self.data.index_select(0, perm), lab
 
     def __iter__(self):
         # one batch per iterator, as DataLoader(batch_size=len(dataset)) yields
         yield self.sample()
 
     def label_matrix(self, labels=None) -> torch.Tensor:
-        """One-hot float32 label matrix of a draw (FullySup.py:153)."""
-        lab = self.labels if labels is None else labels
-        return torch.nn.functional.one_hot(lab, num_classes=self.num_classes).float()
+        """One-hot float32 label matrix of a draw (FullySup.py:153).  Without `labels`: the
+        labels of the latest draw, in that draw's order, so the rows line up with the images
+        `next(iter(provider))` returned; before any draw that is an error (the stored order
+        matches no batch the caller holds)."""
+        if labels is None:
+            if self._last_labels is None:
+                raise RuntimeError("label_matrix(): no draw yet -- pass the labels of the batch")
+            labels = self._last_labels
+        return torch.nn.functional.one_hot(labels, num_classes=self.num_classes).float()

@@ -531,7 +531,12 @@ constexpr int kOob = 0x7FFFFFF0;   // buffer offset past any num_records: the lo
 // rows grp, grp + NG, ...); lane li of the group owns column quad li (columns 4li..4li+3) of
 // those rows and keeps x, r, u, w, p, s, q, z for them in registers for the whole solve.
 // The group's lanes split each row's entries for the gathers and sum them by DPP.
-template <class Mat, int NT, int LPR, int RPG>
+// MODE 0: pipelined PCG (Ghysels-Vanroose), one grid barrier per iteration.  MODE 1:
+// Chronopoulos-Gear single-reduction PCG on the same machinery, two barriers per iteration
+// (u published, then the partials): its recurrences keep fp32 attainable accuracy close to
+// classic PCG's, where GV's drift on ill-conditioned systems -- utils.laplace's tau = 1e-8 at
+// 60,250 points took 303 GV iterations against 92 (profiles/r03c_laplace_probe.txt).
+template <class Mat, int NT, int LPR, int RPG, int MODE>
 __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
     GLL_TRACE_SCOPE(1);
     extern __shared__ __attribute__((aligned(16))) int2 s_ent[];   // (byte offset, value bits)
@@ -681,12 +686,14 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
     }
     unsigned epoch = 0;
     bool ok = gv_barrier(a.sync, ++epoch, G, a.hier, &s_ok);
+    if constexpr (MODE == 0) {
 #pragma unroll
-    for (int k = 0; k < RPG; ++k) {
-        const int uu = r0 + grp + k * NG;
-        if (uu < r1) {
-            const f32x4 o = spmv(k, rv0);
-            w[k] = Mat::kSeparateDiag ? dg[k] * u[k] + o : o;
+        for (int k = 0; k < RPG; ++k) {
+            const int uu = r0 + grp + k * NG;
+            if (uu < r1) {
+                const f32x4 o = spmv(k, rv0);
+                w[k] = Mat::kSeparateDiag ? dg[k] * u[k] + o : o;
+            }
         }
     }
 
@@ -696,7 +703,18 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
         const int pub = (it + 1) & 1;
         const __amdgpu_buffer_rsrc_t rvp = pub ? rv1 : rv0;
         const __amdgpu_buffer_rsrc_t rpp = pub ? rpt1 : rpt0;
-        // ---- local: partial (r,u), (w,u), (r,r); publish m = M w
+        if constexpr (MODE == 1) {   // w = A u, u published before the last barrier
+            const __amdgpu_buffer_rsrc_t rvu = pub ? rv0 : rv1;
+#pragma unroll
+            for (int k = 0; k < RPG; ++k) {
+                const int uu = r0 + grp + k * NG;
+                if (uu < r1) {
+                    const f32x4 o = spmv(k, rvu);
+                    w[k] = Mat::kSeparateDiag ? dg[k] * u[k] + o : o;
+                }
+            }
+        }
+        // ---- local: partial (r,u), (w,u), (r,r); publish m = M w (pipelined form)
         {
             f32x4 pg = {0.f, 0.f, 0.f, 0.f}, pd = pg, pr = pg;
 #pragma unroll
@@ -706,8 +724,9 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
                     pg += r[k] * u[k];
                     pd += w[k] * u[k];
                     pr += r[k] * r[k];
-                    __builtin_amdgcn_raw_buffer_store_b128(mi[k] * w[k], rvp, uu * rowB + 16 * li,
-                                                           0, kSc1);
+                    if constexpr (MODE == 0)
+                        __builtin_amdgcn_raw_buffer_store_b128(mi[k] * w[k], rvp,
+                                                               uu * rowB + 16 * li, 0, kSc1);
                 }
             }
             // lanes of one quad across the wave's row groups, then the waves in order
@@ -756,7 +775,7 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
         for (int k = 0; k < RPG; ++k) {
             const int uu = r0 + grp + k * NG;
             nn[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (uu < r1) {
+            if (MODE == 0 && uu < r1) {
                 const f32x4 o = spmv(k, rvp);
                 nn[k] = Mat::kSeparateDiag ? dg[k] * (mi[k] * w[k]) + o : o;
             }
@@ -818,10 +837,9 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
         }
         __syncthreads();
         if (!s_any) break;
-        // ---- local updates (Ghysels-Vanroose recurrences)
-        {
-            const f32x4 al = quad_of(s_alpha, li < kGCM / 4 ? li : 0);
-            const f32x4 be = quad_of(s_beta, li < kGCM / 4 ? li : 0);
+        const f32x4 al = quad_of(s_alpha, li < kGCM / 4 ? li : 0);
+        const f32x4 be = quad_of(s_beta, li < kGCM / 4 ? li : 0);
+        if constexpr (MODE == 0) {   // ---- local updates (Ghysels-Vanroose recurrences)
 #pragma unroll
             for (int k = 0; k < RPG; ++k) {
                 const int uu = r0 + grp + k * NG;
@@ -836,6 +854,19 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
                 u[k] -= al * q[k];
                 w[k] -= al * z[k];
             }
+        } else {   // ---- Chronopoulos-Gear: p, s = A p by recurrence; u = M r published
+#pragma unroll
+            for (int k = 0; k < RPG; ++k) {
+                const int uu = r0 + grp + k * NG;
+                if (uu >= r1 || !qown) continue;
+                p[k] = u[k] + be * p[k];
+                s[k] = w[k] + be * s[k];
+                x[k] += al * p[k];
+                r[k] -= al * s[k];
+                u[k] = mi[k] * r[k];
+                __builtin_amdgcn_raw_buffer_store_b128(u[k], rvp, uu * rowB + 16 * li, 0, kSc1);
+            }
+            ok = gv_barrier(a.sync, ++epoch, G, a.hier, &s_ok);
         }
         ++it;
     }
@@ -1011,11 +1042,11 @@ static hipError_t dispatch_classic(const Mat& A, const GridCgArgs& a, int64_t nn
 }
 
 // ---- pipelined kernel
-template <class Mat, int NT, int LPR, int RPG>
+template <class Mat, int NT, int LPR, int RPG, int MODE>
 static hipError_t launch_gv(const Mat& A, GvArgs a, int G, int64_t nnz, float* ws, hipStream_t s) {
     a.rows_per_wg = (a.m + G - 1) / G;
     G = (a.m + a.rows_per_wg - 1) / a.rows_per_wg;
-    auto fn = cg_gv_kernel<Mat, NT, LPR, RPG>;
+    auto fn = cg_gv_kernel<Mat, NT, LPR, RPG, MODE>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
     // the slice: the workgroup's share of the entries with a quarter of margin (rows beyond it
     // read the CSR), within what the static LDS leaves; unknown nnz (< 0): all of it
@@ -1044,15 +1075,16 @@ static hipError_t launch_gv(const Mat& A, GvArgs a, int G, int64_t nnz, float* w
     if (e != hipSuccess) return e;
     static const bool dbg = getenv("GLL_DEBUG") != nullptr;
     if (dbg)
-        fprintf(stderr, "gll: grid CG (pipelined) G=%d rows/wg=%d NT=%d LPR=%d RPG=%d lds=%zu "
-                "hier=%d\n", G, a.rows_per_wg, NT, LPR, RPG, lds, a.hier);
+        fprintf(stderr, "gll: grid CG (%s) G=%d rows/wg=%d NT=%d LPR=%d RPG=%d lds=%zu hier=%d\n",
+                MODE == 0 ? "pipelined" : "Chronopoulos-Gear", G, a.rows_per_wg, NT, LPR, RPG, lds,
+                a.hier);
     return launch_persistent(fn, G, NT, lds, s, "gridcg.hip:launch_gv", A, a);
 }
 
 // Workgroups: one per CU at most, about 16 rows each (GLL_GRID_G overrides, diagnostic);
 // lanes per row as wide as the rows per workgroup allow; up to 512 rows per workgroup (m <=
 // 131,072 at 256 workgroups).  hipErrorNotSupported: no configuration holds it.
-template <class Mat>
+template <class Mat, int MODE>
 static hipError_t dispatch_gv(const Mat& A, const GridCgArgs& c, int64_t nnz, float* ws,
                               hipStream_t s) {
     GvArgs a{};
@@ -1084,16 +1116,16 @@ static hipError_t dispatch_gv(const Mat& A, const GridCgArgs& c, int64_t nnz, fl
     // (16 waves: more gathers in flight per CU) for long row blocks (GLL_GRID_NT overrides)
     const int nt = env_int("GLL_GRID_NT", R <= 64 ? 256 : 1024);
     if (nt == 256) {
-        if (R <= 16) return launch_gv<Mat, 256, 16, 1>(A, a, G, nnz, ws, s);
-        if (R <= 32) return launch_gv<Mat, 256, 8, 1>(A, a, G, nnz, ws, s);
-        if (R <= 64) return launch_gv<Mat, 256, 4, 1>(A, a, G, nnz, ws, s);
-        if (R <= 128) return launch_gv<Mat, 256, 4, 2>(A, a, G, nnz, ws, s);
-        if (R <= 256) return launch_gv<Mat, 256, 4, 4>(A, a, G, nnz, ws, s);
+        if (R <= 16) return launch_gv<Mat, 256, 16, 1, MODE>(A, a, G, nnz, ws, s);
+        if (R <= 32) return launch_gv<Mat, 256, 8, 1, MODE>(A, a, G, nnz, ws, s);
+        if (R <= 64) return launch_gv<Mat, 256, 4, 1, MODE>(A, a, G, nnz, ws, s);
+        if (R <= 128) return launch_gv<Mat, 256, 4, 2, MODE>(A, a, G, nnz, ws, s);
+        if (R <= 256) return launch_gv<Mat, 256, 4, 4, MODE>(A, a, G, nnz, ws, s);
     } else {
-        if (R <= 64) return launch_gv<Mat, 1024, 16, 1>(A, a, G, nnz, ws, s);
-        if (R <= 128) return launch_gv<Mat, 1024, 8, 1>(A, a, G, nnz, ws, s);
-        if (R <= 256) return launch_gv<Mat, 1024, 4, 1>(A, a, G, nnz, ws, s);
-        if (R <= 512) return launch_gv<Mat, 1024, 4, 2>(A, a, G, nnz, ws, s);
+        if (R <= 64) return launch_gv<Mat, 1024, 16, 1, MODE>(A, a, G, nnz, ws, s);
+        if (R <= 128) return launch_gv<Mat, 1024, 8, 1, MODE>(A, a, G, nnz, ws, s);
+        if (R <= 256) return launch_gv<Mat, 1024, 4, 1, MODE>(A, a, G, nnz, ws, s);
+        if (R <= 512) return launch_gv<Mat, 1024, 4, 2, MODE>(A, a, G, nnz, ws, s);
     }
     return hipErrorNotSupported;
 }
@@ -1104,7 +1136,11 @@ template <class Mat>
 static hipError_t dispatch_grid(const Mat& A, const GridCgArgs& a, int64_t nnz, float* ws,
                                 bool oversub, hipStream_t s) {
     if (!oversub && env_int("GLL_GRID_CLASSIC", 0) == 0) {
-        const hipError_t e = dispatch_gv(A, a, nnz, ws, s);
+        // Luu solves (rtol 1e-6 relative): pipelined; general CSR (utils.laplace's refinement
+        // sweeps on ill-conditioned systems): Chronopoulos-Gear.  GLL_GRID_MODE overrides.
+        const int mode = env_int("GLL_GRID_MODE", Mat::kSeparateDiag ? 0 : 1);
+        const hipError_t e = mode == 0 ? dispatch_gv<Mat, 0>(A, a, nnz, ws, s)
+                                       : dispatch_gv<Mat, 1>(A, a, nnz, ws, s);
         if (e != hipErrorNotSupported) return e;
     }
     return dispatch_classic(A, a, nnz < 0 ? int64_t(a.m) * 8 : nnz, ws, oversub, s);

@@ -389,7 +389,7 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     a.Wadj = L.at<float>(ws, L.Wadj);
     a.ell_col = L.at<int32_t>(ws, L.ell_col);
     a.ell_w = L.at<float>(ws, L.ell_w);
-    a.SE = L.SE;
+    a.SE = ell_emit(L, bt.B);
     a.m = L.m;
     a.vr = L.at<char>(ws, L.vr);
     a.VRM = L.VRM;

@@ -1052,9 +1052,10 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
     if (cap > kOvfLds) cap = kOvfLds;
     if (cap < 0) cap = 0;
     lds += size_t(cap) * 8;
-    if (S != L.SE) {   // row_build emitted L.SE slots
+    if (S != ell_emit(L, bt.B)) {   // row_build emitted ell_emit(L, B) slots
         (void)hipGetLastError();
-        if (getenv("GLL_DEBUG")) fprintf(stderr, "gll: run_ell S=%d but ELL width %d\n", S, L.SE);
+        if (getenv("GLL_DEBUG"))
+            fprintf(stderr, "gll: run_ell S=%d but ELL width %d\n", S, ell_emit(L, bt.B));
         return hipErrorInvalidValue;
     }
     auto fn = cg_ell_kernel<NT, R, S, TB, MODE>;
@@ -1126,6 +1127,28 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
         GLL_VR(512, 4, 4); GLL_VR(512, 4, 8); GLL_VR(512, 4, 10);
 #undef GLL_VR
         return hipErrorInvalidValue;
+    }
+    // batched launches: the narrower ELL slice of ell_emit (same thread layout as a single
+    // call, so the sums run in the same order; single-reduction form only)
+    const int se = ell_emit(L, bt.B);
+    if (m <= 512 && se != 24) {
+#define GLL_ELLB(NT_, R_)                                                                   \
+        {                                                                                   \
+            if (se == 8)                                                                    \
+                return run_ell<NT_, R_, 8, TB, 1>(L, bt, ws, b, bs, out64, out32, rtol,     \
+                                                  max_iter, st_nonconv, st_iters, s);       \
+            if (se == 12)                                                                   \
+                return run_ell<NT_, R_, 12, TB, 1>(L, bt, ws, b, bs, out64, out32, rtol,    \
+                                                   max_iter, st_nonconv, st_iters, s);      \
+            if (se == 16)                                                                   \
+                return run_ell<NT_, R_, 16, TB, 1>(L, bt, ws, b, bs, out64, out32, rtol,    \
+                                                   max_iter, st_nonconv, st_iters, s);      \
+        }
+        if (m <= 64) GLL_ELLB(64, 1);
+        if (m <= 128) GLL_ELLB(128, 1);
+        if (m <= 256) GLL_ELLB(256, 1);
+        GLL_ELLB(256, 2);
+#undef GLL_ELLB
     }
     if (m <= 64) GLL_ELL(64, 1, 24);
     if (m <= 128) GLL_ELL(128, 1, 24);

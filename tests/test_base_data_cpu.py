@@ -99,3 +99,18 @@ def test_rejects_misaligned_or_float_labels():
         DeviceBaseLoader(data, labels[:9], device="cpu")
     with pytest.raises(TypeError):
         DeviceBaseLoader(data, labels.float(), device="cpu")
+
+
+def test_label_matrix_default_follows_the_latest_draw():
+    """`Y = p.label_matrix()` right after `imgs, _ = next(iter(p))` lines up with those images
+    (the draw's permuted labels, not the stored order); before any draw it is an error."""
+    import pytest
+    data, labels = _base(50)
+    p = DeviceBaseLoader(data, labels, device="cpu", seed=4)
+    with pytest.raises(RuntimeError):
+        p.label_matrix()
+    imgs, lab = next(iter(p))
+    Y = p.label_matrix()
+    idx = imgs[:, 0, 0, 0].long()                      # sample i of the draw is base row idx[i]
+    assert torch.equal(Y, torch.nn.functional.one_hot(labels[idx], 10).float())
+    assert torch.equal(Y, p.label_matrix(lab))

@@ -59,7 +59,7 @@ def test_workspace_bytes_and_validation():
     bad.K = 1
     assert lib.gll_workspace_bytes(ct.byref(bad)) == 0
     big_k = G.make_problem(1000, 512, 500, 10, 100, 0.07, 1.0)
-    assert lib.gll_workspace_bytes(ct.byref(big_k)) == 0   # K-1 > 64 unsupported
+    assert lib.gll_workspace_bytes(ct.byref(big_k)) == 0   # K - 1 > 56 (kMaxKm1) unsupported
     assert lib.gll_strerror(-2).decode().startswith("unsupported")
 
 
@@ -127,3 +127,17 @@ def test_torch_extension_module_loads():
     ext = GG._ext()
     assert ext is not None, "_gll_torch.so missing: run __graft_entry__.build()"
     assert hasattr(ext, "laplace_learning")
+
+
+def test_k_outside_the_supported_range_raises_a_clear_error():
+    """k (neighbours incl. self) must satisfy 2 <= min(k, n) <= 57 (include/gll.h): the Python
+    layer says so before anything reaches the device."""
+    import torch
+    from graphlearninglayer_amd import GLL
+    X = torch.zeros(100, 8)
+    Y = torch.zeros(10, 3)
+    for k in (1, 58, 100):
+        with pytest.raises(ValueError, match="2 <= min"):
+            GLL.LaplaceLearningSparseHard.apply(X, Y, 0.0, 1.0, k)
+    with pytest.raises(ValueError, match="2 <= min"):
+        GLL.device_graph(X, 64)

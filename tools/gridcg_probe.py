@@ -32,8 +32,10 @@ VARIANTS = {
     "gv_nt1024": {"GLL_GRID_NT": "1024"},
     "gv_nt1024_g64": {"GLL_GRID_NT": "1024", "GLL_GRID_G": "64"},
     "gv_nt1024_g128": {"GLL_GRID_NT": "1024", "GLL_GRID_G": "128"},
+    "mode_pipe": {"GLL_GRID_MODE": "0"},
+    "mode_cg": {"GLL_GRID_MODE": "1"},
 }
-KEYS = ("GLL_GRID_CLASSIC", "GLL_GRID_HIER", "GLL_GRID_G", "GLL_GRID_NT")
+KEYS = ("GLL_GRID_CLASSIC", "GLL_GRID_HIER", "GLL_GRID_G", "GLL_GRID_NT", "GLL_GRID_MODE")
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--variants", default="classic,gv,gv_flat,gv_g128,gv_g64")
