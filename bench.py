@@ -66,6 +66,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=64,
                     help="graphs per launch of the batched entry point measured beside the "
                          "headline (SURVEY.md §8f-2); 0 disables")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="diagnostic: every rank on cuda:0 over gloo (RCCL refuses two ranks on "
+                         "one GPU), to run the real multi-rank GPU leg on a one-GPU box; the "
+                         "JSON line is marked and is no scaling measurement")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU stand-in step over gloo instead of the GPU path (launcher and "
                          "gather test; the JSON line is marked dry_run and is no measurement)")
@@ -109,6 +113,8 @@ def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps):
         "grad_spmm_kernel": ("hbm", (12.0 * E + 8.0 * n * d) if auto_eps
                              else (8.0 * E + 8.0 * n * C + 8.0 * n * d)),
     }
+    # the fused backward of a single small graph (adjoint CG + feature gradient, one launch)
+    u["cg_grad_fused_kernel"] = ("hbm", iters_bwd * b_spmv + u["grad_spmm_kernel"][1])
     return u
 
 
@@ -144,7 +150,8 @@ PMC_SYMBOLS = {"gram_d2_kernel": ["gram_pk_kernel", "gram_bf3s_kernel", "gram_bf
                                    "gram_lds_kernel", "gram_wide_kernel"], "knn_select_kernel": ["knn_select_kernel"],
                "row_build_kernel": ["row_build_kernel"],
                "cg_kernel": ["cg_ell_kernel", "cg_vr_kernel", "cg_grid_kernel", "cg_lds_kernel"],
-               "edge_coef_kernel": ["edge_coef_kernel"], "grad_spmm_kernel": ["grad_spmm_kernel", "grad_chunk_kernel"]}
+               "edge_coef_kernel": ["edge_coef_kernel"], "grad_spmm_kernel": ["grad_spmm_kernel", "grad_chunk_kernel"],
+               "cg_grad_fused_kernel": ["cg_grad_fused_kernel"]}
 
 
 def pmc_traffic(config, kernel):
@@ -413,11 +420,17 @@ def main():
         return 2
     if a.dry_run:
         return dry_run(a, world, rank)
+    if a.share_gpu:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.share_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    coll = torch.device("cpu") if a.share_gpu else dev   # gloo collectives on host tensors
 
     c = dict(CONFIGS[a.config])
     c["n"] = c["base"] + c["batch"]
@@ -477,7 +490,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -485,9 +498,10 @@ def main():
     if world > 1:
         # every rank's inputs are fixed, so each slot of the last gathered group must hold
         # that rank's U: compare per-rank checksums (one tiny all_gather, outside the timing)
-        own = U.detach().double().sum().reshape(1)
-        sums = torch.empty(world, dtype=torch.float64, device=dev)
+        own = U.detach().double().sum().reshape(1).to(coll)
+        sums = torch.empty(world, dtype=torch.float64, device=coll)
         dist.all_gather_into_tensor(sums, own)
+        sums = sums.to(dev)
         blk = gatherer.gathered[-1].double().sum(dim=(2, 3))            # (world, calls)
         gather_check = "ok" if torch.allclose(blk, sums[:, None].expand_as(blk),
                                               rtol=1e-12, atol=0.0) else "FAILED"
@@ -570,7 +584,9 @@ def main():
             "config": {"workload": a.config, "base": c["base"], "batch": c["batch"], "d": c["d"],
                        "k": k, "eps": eps, "tau": tau, "classes": 10,
                        "parallelism": f"dp{world}", "upstream_grad": "fixed seeded dL/dU",
-                       "collective": (f"async all_gather(U) over RCCL, one per {GATHER_EVERY} calls"
+                       "collective": (("gloo all_gather(U) staged through the host, one per "
+                                       f"{GATHER_EVERY} calls" if a.share_gpu else
+                                       f"async all_gather(U) over RCCL, one per {GATHER_EVERY} calls")
                                       if world > 1 else "none")},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -592,6 +608,10 @@ def main():
                                "frac": round(call_roof_s["split_bf16"] / step_s, 5)}}
         if cpu:
             out["speedup_vs_cpu"] = round(out["value"] / cpu["value"], 1)
+        if a.share_gpu:
+            out["share_gpu"] = (f"DIAGNOSTIC: all {world} ranks ran on cuda:0 over gloo -- the "
+                                "real apply / gather / timed-region code of the multi-rank leg on "
+                                "a one-GPU box; value is not a scaling measurement")
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -28,13 +28,14 @@ FLAG_CG_VR = 1024   # gll_problem.flags: balanced (virtual-row) per-column CG wh
 FLAG_GRAD_ROWS = 2048   # gll_problem.flags: whole-row feature-gradient kernel (diagnostic)
 FLAG_GRAD_CHUNK = 4096  # gll_problem.flags: feature-chunked gradient kernel wherever it runs
 FLAG_GRAM_INLINE = 8192  # gll_problem.flags: 128-tile Gram with the inline split (diagnostic)
+FLAG_BWD_UNFUSED = 16384  # gll_problem.flags: adjoint CG and gradient as two launches (diagnostic)
 ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
 ST_KNN_RESCAN = 5   # kNN rows re-ranked over every column under the Gram error bound
 ST_SOLVE_FAILED = 6   # a whole-GPU CG lost a grid barrier: outputs NaN, raised as an error
 ST_KNN_MERGE = 7   # kNN rows that took the exact candidate merge (diagnostic)
 ST_NWORDS = 16
 K_GRAM, K_SELECT, K_FINALIZE, K_CG, K_EDGE, K_GRAD = range(6)
-K_COUNT = 6
+K_COUNT = 7
 
 # every symbol include/gll.h declares (tests check the library exports all of them)
 EXPORTS = (

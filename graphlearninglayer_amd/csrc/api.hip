@@ -79,7 +79,7 @@ hipError_t launch_status(const char* what) {
 
 static const char* kKernelNames[GLL_K_COUNT] = {
     "gram_d2_kernel", "knn_select_kernel", "row_build_kernel",
-    "cg_kernel",      "edge_coef_kernel",  "grad_spmm_kernel"};
+    "cg_kernel",      "edge_coef_kernel",  "grad_spmm_kernel", "cg_grad_fused_kernel"};
 
 static bool vec_ok(const float* X, int d) {
     return (d % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
@@ -170,12 +170,19 @@ static int backward_impl(const gll_problem* p, int B, const float* X, void* ws,
     const int max_iter = p->max_iter > 0 ? p->max_iter : 1000;
     int32_t* st = public_status(p, L, ws);
     float* wU = L.at<float>(ws, L.Wadj) + size_t(L.base) * L.C;
+    const bool auto_eps = !(p->eps > 0.f);
+    if (B == 1 && !auto_eps) {   // one small graph: adjoint CG + gradient in one launch
+        const hipError_t e = launch_cg_grad_fused(L, ws, gbar, g_dtype, X, p->eps, gradX, rtol,
+                                                  max_iter, st + GLL_ST_BWD_NONCONV,
+                                                  st + GLL_ST_BWD_ITERS, st + GLL_ST_SOLVE_FAILED,
+                                                  vec_ok(X, p->d), s);
+        if (e != hipErrorNotSupported) return hip_status(e);
+    }
     // adjoint solve: Luu is symmetric, so Luu^-T gbar = Luu^-1 gbar (GLL.py:93)
     hipError_t e = launch_cg_luu(L, bt, ws, gbar, bt.g, g_dtype, nullptr, wU, rtol, max_iter,
                                  st + GLL_ST_BWD_NONCONV, st + GLL_ST_BWD_ITERS,
                                  st + GLL_ST_SOLVE_FAILED, s);
     if (e != hipSuccess) return GLL_ERR_HIP;
-    const bool auto_eps = !(p->eps > 0.f);
     return hip_status(launch_backward_grad(L, bt, ws, X, auto_eps, p->eps, gradX,
                                            vec_ok(X, p->d), s));
 }

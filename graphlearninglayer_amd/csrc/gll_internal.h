@@ -158,6 +158,7 @@ struct Layout {
     size_t vr;        // [m][VRM] packed virtual rows (kVrSlot bytes each)
     int dp;           // split-Gram planes: d rounded up to 64
     size_t xhi, xlo, xnrm;   // [n][dp] bf16 hi / lo planes of x - x_0, and |x - x_0|^2
+    size_t fsync;     // fused backward: [0] solved columns, [32] finished gradient blocks
 
     explicit Layout(const gll_problem& p) {
         n = p.n; d = p.d; base = p.base; C = p.C;
@@ -205,6 +206,7 @@ struct Layout {
         xhi = take(size_t(n) * dp * 2);
         xlo = take(size_t(n) * dp * 2);
         xnrm = take(size_t(n) * 4);
+        fsync = take(256);   // two counters on their own 128-B lines, zeroed by row_build
         P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)
         Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
         S = take(size_t(Etot) * 4);        // per-edge coefficient (auto eps / chunked gradient)
@@ -547,5 +549,11 @@ hipError_t launch_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* co
 hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, const float* X,
                                 bool auto_eps, float eps_fixed, float* gradX, bool vec,
                                 hipStream_t s);
+// One small graph, fixed eps: the adjoint CG and the feature gradient in one launch
+// (solve.hip cg_grad_fused_kernel); hipErrorNotSupported when the shape does not qualify.
+hipError_t launch_cg_grad_fused(const Layout& L, void* ws, const void* gbar, int g_dtype,
+                                const float* X, float eps_fixed, float* gradX, float rtol,
+                                int max_iter, int32_t* st_nonconv, int32_t* st_iters,
+                                int32_t* st_failed, bool vec, hipStream_t s);
 
 }  // namespace gll

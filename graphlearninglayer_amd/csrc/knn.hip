@@ -1446,6 +1446,178 @@ void knn_select_kernel(
     }
 }
 
+// --------------------------------------------------------------------------------------
+// gram_pk2_kernel (round 3): the pre-split bf16 GEMM on 256 x 256 upper-triangle tiles with 8
+// waves -- two per SIMD -- of 64 x 128 (2 x 4 accumulators of 32 x 32), k-stages of 32 features.
+// gram_pk_kernel's 128-tile moves 64 KiB into the CU per 48 MFMAs per wave at one wave per
+// SIMD (~96 flops per staged byte; MFMA busy 25-28%, profiles/r02f_mfma_*.json): the CU's
+// L2 -> LDS rate, not the matrix pipe, set its pace.  Here a stage is the same 64 KiB (A hi /
+// lo and B hi / lo, 256 rows x 64 B each, by LDS-DMA, double-buffered: 128 KiB) for 48 MFMAs
+// on EACH of 8 waves -- twice the flops per byte -- and the second wave per SIMD covers the
+// other's waits.  Rows are 64 B in LDS, the four 16-B segments XOR-swizzled by (row >> 2) & 3 on
+// the source address, which keeps every ds_read_b128 lane group of a fragment read on 16
+// distinct bank groups.  Same k order per element as gram_pk_kernel (16-feature chunks in
+// ascending order, lo*hi, hi*lo, hi*hi), same epilogue formula, same upper-triangle values
+// stored in both orientations: D2 is bitwise gram_pk_kernel's.
+// --------------------------------------------------------------------------------------
+constexpr int kPK2 = 32;   // features per k-stage of the 256-tile kernel
+
+__global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict__ Ph,
+                                                       const __bf16* __restrict__ Pl,
+                                                       const float* __restrict__ nrm, int n,
+                                                       int dp, int T, float* __restrict__ D2,
+                                                       int ld, size_t wss) {
+    const int NT = T * (T + 1) / 2;
+    const int idx = xcd_tile(blockIdx.x, gridDim.x);
+    const int g = idx / NT;
+    {
+        const size_t off = size_t(g) * wss;   // graph g's workspace block
+        Ph = reinterpret_cast<const __bf16*>(reinterpret_cast<const char*>(Ph) + off);
+        Pl = reinterpret_cast<const __bf16*>(reinterpret_cast<const char*>(Pl) + off);
+        nrm = reinterpret_cast<const float*>(reinterpret_cast<const char*>(nrm) + off);
+        D2 = reinterpret_cast<float*>(reinterpret_cast<char*>(D2) + off);
+    }
+    constexpr int kTP = 256 * kPK2;                                 // bf16 per tile plane
+    __shared__ __attribute__((aligned(16))) __bf16 sm[2 * 4 * kTP];  // 128 KiB: [buf][plane]
+    const int lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    int bi, bj;
+    supertile_tile(idx - g * NT, T, bi, bj);
+    const int wr = w >> 1, wc = w & 1;   // rows wr * 64 .., columns wc * 128 ..
+    // DMA pieces of a stage: 4 planes x 16 chunks of 16 rows (1 KiB each); wave w issues pieces
+    // q = 0..7: plane q >> 1, chunk (q & 1) * 8 + w; lane -> row 16 c + lane / 4, LDS segment
+    // lane % 4 <- source segment (lane % 4) ^ ((row >> 2) & 3)
+    const __bf16* src[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int pl = q >> 1, c = (q & 1) * 8 + w;
+        const int row = 16 * c + (lane >> 2);
+        const int seg = (lane & 3) ^ ((row >> 2) & 3);
+        int grow = (pl < 2 ? bi : bj) * 256 + row;
+        grow = grow < n ? grow : n - 1;
+        src[q] = ((pl & 1) ? Pl : Ph) + size_t(grow) * dp + 8 * seg;
+    }
+    auto issue4 = [&](int ks, int buf, int q0) {
+#pragma unroll
+        for (int q = q0; q < q0 + 4; ++q) {
+            const int pl = q >> 1, c = (q & 1) * 8 + w;
+            __bf16* dst = sm + (buf * 4 + pl) * kTP + c * 16 * kPK2;
+            __builtin_amdgcn_global_load_lds(src[q] + ks * kPK2, (lds_void*)dst, 16, 0, 0);
+        }
+    };
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+    auto frag = [&](int buf, int pl, int row, int kk) {
+        const int pos = (2 * kk + h) ^ ((row >> 2) & 3);
+        return *reinterpret_cast<const bf16x8*>(sm + (buf * 4 + pl) * kTP + row * kPK2 + 8 * pos);
+    };
+    const int nks = dp / kPK2;
+    issue4(0, 0, 0);
+    issue4(0, 0, 4);
+    for (int ks = 0; ks < nks; ++ks) {
+        const int buf = ks & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's stage-ks DMAs
+        __builtin_amdgcn_s_barrier();                          // every wave's
+        const bool more = ks + 1 < nks;
+#pragma unroll
+        for (int kk = 0; kk < kPK2 / 16; ++kk) {
+            if (more) issue4(ks + 1, buf ^ 1, 4 * kk);
+            bf16x8 ah[2], al[2], bh[4], bl[4];
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                ah[m] = frag(buf, 0, wr * 64 + m * 32 + r, kk);
+                al[m] = frag(buf, 1, wr * 64 + m * 32 + r, kk);
+            }
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                bh[m] = frag(buf, 2, wc * 128 + m * 32 + r, kk);
+                bl[m] = frag(buf, 3, wc * 128 + m * 32 + r, kk);
+            }
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+                }
+        }
+    }
+    // epilogue: D2 = |a_i|^2 + |a_j|^2 - 2 <a_i, a_j>; C layout of 32x32: col = lane & 31,
+    // row = (e & 3) + 8 (e >> 2) + 4 h.  Diagonal tiles keep the upper triangle (tj >= ti, the
+    // value gram_pk_kernel stores there) and write it in both orientations.
+    const bool diag = bi == bj;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        const int ti0 = wr * 64 + a * 32;
+        const int i0 = bi * 256 + ti0;
+        float ni[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int i = i0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            ni[e] = nrm[i < n ? i : n - 1];
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int tj = wc * 128 + b * 32 + r;
+            const int j = bj * 256 + tj;
+            if (diag && wc * 128 + b * 32 + 31 < ti0) continue;   // sub-tile wholly below
+            const float nj = nrm[j < n ? j : n - 1];
+            float dv[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) dv[e] = ni[e] + nj - 2.f * acc[a][b][e];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {   // direct: 32 lanes per 128-B row piece
+                const int ti = ti0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                const int i = bi * 256 + ti;
+                if (i < n && j < n && (!diag || tj >= ti)) D2[size_t(i) * ld + j] = dv[e];
+            }
+            if (j < n) {   // mirrored: row j, columns i0 + 8 g + 4 h .. +3
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    const int ti = ti0 + 8 * gq + 4 * h;
+                    const int i = bi * 256 + ti;
+                    float* dst = D2 + size_t(j) * ld + i;
+                    if (i + 4 <= n && (!diag || tj >= ti + 3)) {
+                        *reinterpret_cast<f32x4*>(dst) =
+                            f32x4{dv[4 * gq], dv[4 * gq + 1], dv[4 * gq + 2], dv[4 * gq + 3]};
+                    } else {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            if (i + t < n && (!diag || tj >= ti + t)) dst[t] = dv[4 * gq + t];
+                    }
+                }
+            }
+        }
+    }
+}
+
+// 256-tiles (gram_pk2_kernel) or 128-tiles (gram_pk_kernel) for the pre-split GEMM: the one
+// with fewer waves of one-workgroup-per-CU rounds x k-stage bytes (a round of 256-tiles moves
+// the same 64 KiB per stage as one of 128-tiles but does 4x the work, in twice the stages).
+// GLL_GRAM_TILE = 128 / 256 forces one (diagnostic A/B).
+static bool gram_tile256(const Layout& L, const Batch& bt, int T, int T2) {
+    const char* e = getenv("GLL_GRAM_TILE");
+    if (e) return atoi(e) == 256;
+    if (L.dp % kPK2) return false;
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, v = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+        cus = v > 0 ? v : 256;
+    }
+    const int64_t t1 = int64_t(bt.B) * T * (T + 1) / 2, t2 = int64_t(bt.B) * T2 * (T2 + 1) / 2;
+    const int64_t r1 = (t1 + cus - 1) / cus, r2 = (t2 + cus - 1) / cus;
+    return r2 * 2 * (L.dp / kPK2) * kPK2 < r1 * (L.dp / kPK) * kPK;   // stage bytes equal
+}
+
 hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
                        hipStream_t s) {
     float* D2 = L.at<float>(ws, L.D2);
@@ -1489,8 +1661,13 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
             launch_k(gram_split_kernel<true>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
         else
             launch_k(gram_split_kernel<false>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
-        launch_k(gram_pk_kernel, dim3(unsigned(bt.B * T * (T + 1) / 2)), 256, 0, s, Ph, Pl, nrm,
-                 L.n, L.dp, T, D2, L.ldD, bt.ws);
+        const int T2 = (L.n + 255) / 256;
+        if (gram_tile256(L, bt, T, T2))
+            launch_k(gram_pk2_kernel, dim3(unsigned(bt.B * T2 * (T2 + 1) / 2)), 512, 0, s, Ph,
+                     Pl, nrm, L.n, L.dp, T2, D2, L.ldD, bt.ws);
+        else
+            launch_k(gram_pk_kernel, dim3(unsigned(bt.B * T * (T + 1) / 2)), 256, 0, s, Ph, Pl,
+                     nrm, L.n, L.dp, T, D2, L.ldD, bt.ws);
         prof_end(GLL_K_GRAM, s);
         return launch_status("knn.hip:launch_gram(pk)");
     }

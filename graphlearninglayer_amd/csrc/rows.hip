@@ -55,6 +55,7 @@ struct RowArgs {
     int SE, m;
     char* vr;           // [m][VRM] packed virtual rows of the balanced CG (VRM = 0: none)
     int VRM;
+    unsigned* fsync;    // fused backward counters (solve.hip cg_grad_fused_kernel): zeroed here
     size_t wss;   // batched launches: workspace stride between graphs (bytes)
 
     template <bool FLAT>
@@ -83,6 +84,7 @@ struct RowArgs {
         ell_col = FLAT ? gshift_flat_at(ell_col, wss, g) : gshift_at(ell_col, wss, g);
         ell_w = FLAT ? gshift_flat_at(ell_w, wss, g) : gshift_at(ell_w, wss, g);
         vr = FLAT ? gshift_flat_at(vr, wss, g) : gshift_at(vr, wss, g);
+        fsync = FLAT ? gshift_flat_at(fsync, wss, g) : gshift_at(fsync, wss, g);
     }
 };
 
@@ -320,6 +322,10 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
     const int wv = threadIdx.x >> 6;
     const int i = gxy.x * 4 + wv;
     if (i >= a.n) return;
+    if (i == 0 && lane == 0) {   // the backward's hand-off counters start at zero
+        a.fsync[0] = 0u;
+        a.fsync[32] = 0u;
+    }
     const int Km1 = a.K - 1;
     int fi = -1;
     float fd = 0.f;
@@ -393,6 +399,7 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     a.m = L.m;
     a.vr = L.at<char>(ws, L.vr);
     a.VRM = L.VRM;
+    a.fsync = L.at<unsigned>(ws, L.fsync);
     a.wss = bt.ws;
     dim3 grid((L.n + 3) / 4, bt.B);
     prof_begin(GLL_K_FINALIZE, s);

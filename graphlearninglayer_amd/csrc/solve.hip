@@ -28,6 +28,7 @@
 #include <unordered_set>
 
 #include "gll_internal.h"
+#include "grad_common.h"
 
 namespace gll {
 
@@ -35,6 +36,7 @@ GLL_TRACE_UNIT(solve)
 
 static constexpr size_t kLdsLimit = 160 * 1024;
 static constexpr size_t kLdsDyn = kLdsLimit - 1024;   // dynamic share, room for static LDS
+constexpr int kSc1W = 16;   // buffer aux bit sc1 (write-through / L2-coherent)
 
 // Opt a kernel into all of the 160 KiB of LDS its static allocation leaves for dynamic use,
 // once per kernel (host-side cost).  The attribute call's status is consumed here: a failure
@@ -190,8 +192,13 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int& total) 
 
 // MODE: 0 classic PCG (two reductions), 1 Chronopoulos-Gear (one reduction, two barriers),
 // 2 pipelined PCG (Ghysels-Vanroose: one barrier per iteration).
+// The kernel body: `gxy` = (column, graph); `fsync` (the fused backward, cg_grad_fused_kernel)
+// non-null: the solution is stored write-through (sc1) and, once every wave has drained its
+// stores, thread 0 adds 1 to fsync[0] -- the feature-gradient workgroups of the same launch
+// wait for C arrivals (MI355X_MICROARCH.md 'Valid forms', first table row).
 template <int NT, int R, int S, typename TB, int MODE>
-__global__ __launch_bounds__(NT) void cg_ell_kernel(
+__device__ __forceinline__ void cg_ell_body(
+    int2 gxy, unsigned* fsync,
     int m, int C, int base, const int32_t* __restrict__ row_start,
     const int32_t* __restrict__ row_len, const int32_t* __restrict__ ucnt,
     const int32_t* __restrict__ col, const float* __restrict__ wv, const float* __restrict__ diag,
@@ -201,7 +208,6 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     const float* __restrict__ ell_w, size_t wss, size_t bs,
     size_t us, size_t sts) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int2 gxy = batch_xy<true>();   // once: per pointer it re-reads gridDim and divides
     ell_col = gshift_at(ell_col, wss, gxy.y);
     ell_w = gshift_at(ell_w, wss, gxy.y);
     row_start = gshift_br_at(row_start, wss, gxy.y);   // batched launches: graph blockIdx.y
@@ -629,14 +635,43 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
         const int u = urow[q];
         if (u < m) {
             if (out64) out64[size_t(u) * C + c] = double(x[q]);
-            if (out32) out32[size_t(u) * C + c] = x[q];
+            if (out32) {
+                if (fsync)
+                    __hip_atomic_store(out32 + size_t(u) * C + c, x[q], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);   // global_store ... sc1
+                else
+                    out32[size_t(u) * C + c] = x[q];
+            }
         }
     }
     if (tid == 0) {
         if (st_iters) atomicMax(st_iters, it);
         if (!conv && st_nonconv) atomicAdd(st_nonconv, 1);
     }
+    if (fsync) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+            __hip_atomic_fetch_add(fsync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     GLL_TRACE_PT(9);
+}
+
+template <int NT, int R, int S, typename TB, int MODE>
+__global__ __launch_bounds__(NT) void cg_ell_kernel(
+    int m, int C, int base, const int32_t* __restrict__ row_start,
+    const int32_t* __restrict__ row_len, const int32_t* __restrict__ ucnt,
+    const int32_t* __restrict__ col, const float* __restrict__ wv, const float* __restrict__ diag,
+    const TB* __restrict__ bsrc, double* __restrict__ out64, float* __restrict__ out32,
+    float rtol, int max_iter, int mat_cap, int32_t* __restrict__ st_nonconv,
+    int32_t* __restrict__ st_iters, const int32_t* __restrict__ ell_col,
+    const float* __restrict__ ell_w, size_t wss, size_t bs,
+    size_t us, size_t sts) {
+    // batch_xy once: per pointer it re-reads gridDim and divides
+    cg_ell_body<NT, R, S, TB, MODE>(batch_xy<true>(), nullptr, m, C, base, row_start, row_len,
+                                    ucnt, col, wv, diag, bsrc, out64, out32, rtol, max_iter,
+                                    mat_cap, st_nonconv, st_iters, ell_col, ell_w, wss, bs, us,
+                                    sts);
 }
 
 // --------------------------------------------------------------------------------------
@@ -1066,6 +1101,276 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
         L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, int(cap), st_nonconv, st_iters,
         L.at<int32_t>(ws, L.ell_col), L.at<float>(ws, L.ell_w), bt.ws, bs, bt.u, bt.st);
     return launch_status("solve.hip:run_ell");
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused backward of one small graph (gll_backward, B = 1, fixed eps, C = 10, m <= 512: the
+// north-star shape).  The adjoint solve occupies C workgroups of the GPU for ~15 us while the
+// feature gradient waits behind a kernel boundary: dispatch, a gap and then cold loads of X
+// rows, the CSR and P.  Here both run in ONE launch: blocks 0..C-1 are the per-column CG
+// (cg_ell_body), blocks C.. the whole-row gradient (grad_spmm_kernel's register form, one wave
+// per row).  A gradient wave loads everything that does not depend on the solve -- x_i, its
+// edges, P_i and P_j, the first EB neighbour rows x_j -- then waits for the C columns (one
+// counter, the columns' solution stored write-through), loads w_i, w_j with sc1 loads and
+// finishes: the same fma order as grad_spmm_kernel, so the results agree bitwise.  All
+// C + n / (NT / 64) workgroups are co-resident (checked against the occupancy at launch), so
+// a waiting gradient wave never holds a CU a solve needs.  The last gradient workgroup
+// re-arms the counters for the next backward on the same workspace.
+struct EllCgArgs {
+    int m, C, base;
+    const int32_t* row_start;
+    const int32_t* row_len;
+    const int32_t* ucnt;
+    const int32_t* col;
+    const float* wv;
+    const float* diag;
+    const void* b;
+    float* out32;
+    float rtol;
+    int max_iter, mat_cap;
+    int32_t* st_nonconv;
+    int32_t* st_iters;
+    const int32_t* ell_col;
+    const float* ell_w;
+};
+
+template <int NT, int S, typename TB, int ND>
+__global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs a,
+                                                           const float* __restrict__ X,
+                                                           float* __restrict__ out,
+                                                           unsigned* fsync, int32_t* st_failed,
+                                                           int poll_sleep) {
+    const int C = c.C;
+    if (int(blockIdx.x) < C) {
+        cg_ell_body<NT, 1, S, TB, 1>(int2{int(blockIdx.x), 0}, fsync, c.m, C, c.base,
+                                     c.row_start, c.row_len, c.ucnt, c.col, c.wv, c.diag,
+                                     static_cast<const TB*>(c.b), nullptr, c.out32, c.rtol,
+                                     c.max_iter, c.mat_cap, c.st_nonconv, c.st_iters, c.ell_col,
+                                     c.ell_w, 0, 0, 0, 0);
+        return;
+    }
+    // ---- gradient role: one wave per row (C = 10 classes, fixed eps)
+    constexpr int NC = 10;
+    constexpr int EB = ND <= 2 ? 16 : 8;   // grad_spmm_kernel's single-graph (WIDE) batch
+    __shared__ int s_ok;
+    const int lane = lane_id();
+    const int i0 = (int(blockIdx.x) - C) * (NT / kWave) + (threadIdx.x >> 6);
+    const bool live = i0 < a.n;
+    const int i = live ? i0 : 0;
+    const int d = a.d;
+    const int beg = a.row_start[i];
+    const int end = live ? beg + a.row_len[i] : beg;
+    const float ei = a.eps_fixed;
+    const float* xi = X + size_t(i) * d;
+    f32x4 xv[ND];
+#pragma unroll
+    for (int q = 0; q < ND; ++q) xv[q] = load4<true>(xi, 4 * lane + 4 * kWave * q, d);
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    float pi[NC];
+#pragma unroll
+    for (int q = 0; q < NC; q += 2) {
+        const f32x2 v = *reinterpret_cast<const f32x2*>(a.P + size_t(i) * NC + q);
+        pi[q] = v.x, pi[q + 1] = v.y;
+    }
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.Wadj), 0, a.n * NC * 4, 0x00020000);
+    // edge e's neighbour, weight and P row (forward data: plain loads)
+    auto edge_pre = [&](int e, int& cj, float& we, float* pj) {
+        const bool el = e < end;
+        cj = el ? a.col[e] : i;
+        we = el ? a.w[e] : 0.f;
+#pragma unroll
+        for (int q = 0; q < NC; q += 2) {
+            const f32x2 v = *reinterpret_cast<const f32x2*>(a.P + size_t(cj) * NC + q);
+            pj[q] = v.x, pj[q + 1] = v.y;
+        }
+    };
+    // its coefficient once w is complete (edge_gv_r's order)
+    float wi[NC];
+    auto edge_coef = [&](int e, int cj, float we, const float* pj) -> float {
+        float wj[NC];
+#pragma unroll
+        for (int q = 0; q < NC; ++q)
+            wj[q] = __builtin_bit_cast(
+                float, __builtin_amdgcn_raw_buffer_load_b32(rw, (cj * NC + q) * 4, 0, kSc1W));
+        float g = 0.f;
+#pragma unroll
+        for (int q = 0; q < NC; ++q) g = __builtin_fmaf(wi[q] - wj[q], pj[q] - pi[q], g);
+        const float ej = a.eps_fixed;
+        const float v = -8.f * we / (ei * ej);   // GLL.py:217/234
+        return e < end ? g * v : 0.f;
+    };
+    int cj;
+    float we, pj[NC];
+    edge_pre(beg + lane, cj, we, pj);
+    const int cnt0 = min(kWave, end - beg);
+    f32x4 v[EB][ND];
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+        const int t = u < cnt0 ? u : 0;
+        const float* xj = X + size_t(readlane_i(cj, t)) * d;
+#pragma unroll
+        for (int q = 0; q < ND; ++q) v[u][q] = load4<true>(xj, 4 * lane + 4 * kWave * q, d);
+    }
+    // ---- wait for the C column solves (bounded: a lost solve surfaces as NaN + status)
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        unsigned spins = 0;
+        // ~n_poll x 256 cycles between polls: 125 workgroups polling the line the solves add
+        // to would otherwise queue those adds behind a storm of loads
+        while (__hip_atomic_load(fsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+               unsigned(C)) {
+            for (int q = 0; q < poll_sleep; ++q) __builtin_amdgcn_s_sleep(4);
+            if (++spins > (1u << 24)) {
+                ok = 0;
+                break;
+            }
+        }
+        s_ok = ok;
+    }
+    __syncthreads();
+    const bool ok = s_ok != 0;
+#pragma unroll
+    for (int q = 0; q < NC; ++q)
+        wi[q] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rw, (i * NC + q) * 4, 0, kSc1W));
+    f32x4 acc[ND];
+#pragma unroll
+    for (int q = 0; q < ND; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int e0 = beg; e0 < end; e0 += kWave) {
+        if (e0 != beg) edge_pre(e0 + lane, cj, we, pj);   // rows past 64 edges (hubs)
+        const float cf = edge_coef(e0 + lane, cj, we, pj);
+        const int cnt = min(kWave, end - e0);
+        for (int t0 = 0; t0 < cnt; t0 += EB) {
+            float sv[EB];
+            if (e0 != beg || t0 != 0) {
+#pragma unroll
+                for (int u = 0; u < EB; ++u) {
+                    const int t = t0 + u < cnt ? t0 + u : t0;
+                    const float* xj = X + size_t(readlane_i(cj, t)) * d;
+#pragma unroll
+                    for (int q = 0; q < ND; ++q) v[u][q] = load4<true>(xj, 4 * lane + 4 * kWave * q, d);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < EB; ++u) {
+                const int t = t0 + u < cnt ? t0 + u : t0;
+                sv[u] = t0 + u < cnt ? readlane_f(cf, t) : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < EB; ++u) {
+#pragma unroll
+                for (int q = 0; q < ND; ++q) acc[q] += sv[u] * (xv[q] - v[u][q]);
+            }
+        }
+    }
+    if (live) {
+        const float nanf_ = __builtin_nanf("");
+        float* oi = out + size_t(i) * d;
+#pragma unroll
+        for (int q = 0; q < ND; ++q) {
+            const int k = 4 * lane + 4 * kWave * q;
+            const f32x4 r = ok ? acc[q] : f32x4{nanf_, nanf_, nanf_, nanf_};
+            if (k < d) __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(oi + k));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {   // the last gradient workgroup re-arms the counters
+        const unsigned ng = gridDim.x - unsigned(C);
+        const unsigned old = __hip_atomic_fetch_add(fsync + 32, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1u == ng) {
+            __hip_atomic_store(fsync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(fsync + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!ok && st_failed) atomicOr(st_failed, 1);
+    }
+}
+
+template <int NT, int ND, typename TB>
+static hipError_t run_fused(const Layout& L, void* ws, const TB* b, const float* X,
+                            float eps_fixed, float* gradX, float rtol, int max_iter,
+                            int32_t* st_nonconv, int32_t* st_iters, int32_t* st_failed,
+                            hipStream_t s) {
+    constexpr int S = 24;
+    size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4;
+    const int64_t eu_bound = int64_t(L.m + L.n) * (L.K - 1);
+    int64_t cap = int64_t(kLdsDyn - lds) / 8;
+    if (cap > eu_bound) cap = eu_bound;
+    if (cap < 0) cap = 0;
+    lds += size_t(cap) * 8;
+    auto fn = cg_grad_fused_kernel<NT, S, TB, ND>;
+    allow_full_lds(reinterpret_cast<const void*>(fn));
+    const int G = L.C + (L.n + NT / kWave - 1) / (NT / kWave);
+    int nb = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(fn), NT,
+                                                     lds) != hipSuccess)
+        nb = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetLastError();
+    if (int64_t(nb) * cus < G) return hipErrorNotSupported;   // not co-resident: two launches
+    EllCgArgs c;
+    c.m = L.m;
+    c.C = L.C;
+    c.base = L.base;
+    c.row_start = L.at<int32_t>(ws, L.row_start);
+    c.row_len = L.at<int32_t>(ws, L.row_len);
+    c.ucnt = L.at<int32_t>(ws, L.ucnt);
+    c.col = L.at<int32_t>(ws, L.col);
+    c.wv = L.at<float>(ws, L.w);
+    c.diag = L.at<float>(ws, L.diag);
+    c.b = b;
+    c.out32 = L.at<float>(ws, L.Wadj) + size_t(L.base) * L.C;
+    c.rtol = rtol;
+    c.max_iter = max_iter;
+    c.mat_cap = int(cap);
+    c.st_nonconv = st_nonconv;
+    c.st_iters = st_iters;
+    c.ell_col = L.at<int32_t>(ws, L.ell_col);
+    c.ell_w = L.at<float>(ws, L.ell_w);
+    const EdgeArgs a = make_edge_args(L, 0, ws, eps_fixed);
+    prof_begin(GLL_K_BWD, s);
+    const char* ps = getenv("GLL_FUSED_SLEEP");   // diagnostic A/B of the poll interval
+    const int poll_sleep = ps ? atoi(ps) : 4;
+    launch_k(fn, dim3(unsigned(G)), NT, lds, s, c, a, X, gradX, L.at<unsigned>(ws, L.fsync),
+             st_failed, poll_sleep);
+    prof_end(GLL_K_BWD, s);
+    return launch_status("solve.hip:run_fused");
+}
+
+hipError_t launch_cg_grad_fused(const Layout& L, void* ws, const void* gbar, int g_dtype,
+                                const float* X, float eps_fixed, float* gradX, float rtol,
+                                int max_iter, int32_t* st_nonconv, int32_t* st_iters,
+                                int32_t* st_failed, bool vec, hipStream_t s) {
+    const int m = L.m;
+    if (L.C != 10 || !(eps_fixed > 0.f) || !vec || m < 1 || m > 512 || L.RV != 0 ||
+        ell_emit(L, 1) != 24 || L.d > 1024)
+        return hipErrorNotSupported;
+    if (L.flags & (GLL_FLAG_BWD_UNFUSED | GLL_FLAG_CG_GRID | GLL_FLAG_CG_CLASSIC |
+                   GLL_FLAG_CG_PIPE | GLL_FLAG_GRAD_CHUNK))
+        return hipErrorNotSupported;
+    if (size_t(L.n) * L.d * 4 > (size_t(4) << 20)) return hipErrorNotSupported;   // chunked
+    if (getenv("GLL_CG_NT")) return hipErrorNotSupported;   // diagnostic CG shapes: unfused
+    const int nd = (L.d + 255) / 256;
+#define GLL_FUSED(NT_)                                                                       \
+    {                                                                                        \
+        if (g_dtype == GLL_DT_F32) {                                                         \
+            const float* b = static_cast<const float*>(gbar);                                \
+            if (nd <= 1) return run_fused<NT_, 1>(L, ws, b, X, eps_fixed, gradX, rtol, max_iter, st_nonconv, st_iters, st_failed, s); \
+            if (nd <= 2) return run_fused<NT_, 2>(L, ws, b, X, eps_fixed, gradX, rtol, max_iter, st_nonconv, st_iters, st_failed, s); \
+            return run_fused<NT_, 4>(L, ws, b, X, eps_fixed, gradX, rtol, max_iter, st_nonconv, st_iters, st_failed, s); \
+        }                                                                                    \
+        const double* b = static_cast<const double*>(gbar);                                  \
+        if (nd <= 1) return run_fused<NT_, 1>(L, ws, b, X, eps_fixed, gradX, rtol, max_iter, st_nonconv, st_iters, st_failed, s); \
+        if (nd <= 2) return run_fused<NT_, 2>(L, ws, b, X, eps_fixed, gradX, rtol, max_iter, st_nonconv, st_iters, st_failed, s); \
+        return run_fused<NT_, 4>(L, ws, b, X, eps_fixed, gradX, rtol, max_iter, st_nonconv, st_iters, st_failed, s); \
+    }
+    if (m <= 64) GLL_FUSED(64);
+    if (m <= 128) GLL_FUSED(128);
+    if (m <= 256) GLL_FUSED(256);
+    GLL_FUSED(512);
+#undef GLL_FUSED
 }
 
 template <int NT, int R, int RV, typename TB>

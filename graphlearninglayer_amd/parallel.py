@@ -82,24 +82,32 @@ class PredictionGatherer:
         if self._fill >= self.every:
             self.flush()
 
+    def _host_staged(self, t: torch.Tensor) -> bool:
+        # gloo moves host memory: device blocks go through a host copy (the diagnostic that
+        # runs several ranks on one GPU, bench.py --share-gpu; RCCL is the production path)
+        return t.is_cuda and dist.get_backend(self.group) == "gloo"
+
     def flush(self) -> None:
         if self._block is None or self._fill == 0:
             return
         world = dist.get_world_size(self.group)
         block = self._block[: self._fill]
         self._block, self._fill = None, 0
+        dev = block.device
+        if self._host_staged(block):
+            block = block.cpu()
         # concatenated along dim 0 (the layout every backend accepts), viewed per rank below
         out = torch.empty((world * block.shape[0],) + tuple(block.shape[1:]), dtype=block.dtype,
                           device=block.device)
         work = dist.all_gather_into_tensor(out, block, group=self.group, async_op=True)
-        self.inflight.append((out.view((world,) + tuple(block.shape)), work))
+        self.inflight.append((out.view((world,) + tuple(block.shape)), work, dev))
 
     def wait(self) -> None:
         """Flush the partial group and wait for every issued gather."""
         self.flush()
-        for out, work in self.inflight:
+        for out, work, dev in self.inflight:
             work.wait()
-            self.gathered.append(out)
+            self.gathered.append(out.to(dev))
         self.inflight = []
         if self.keep is not None and len(self.gathered) > self.keep:
             del self.gathered[: len(self.gathered) - self.keep]

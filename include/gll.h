@@ -72,6 +72,8 @@ extern "C" {
                                   * run (d >= 128, d % 4 == 0) (diagnostic) */
 #define GLL_FLAG_GRAM_INLINE 8192 /* 128-tile Gram: split each tile's rows inline (the round-1
                                    * kernel) instead of pre-split planes + LDS-DMA (diagnostic) */
+#define GLL_FLAG_BWD_UNFUSED 16384 /* single small graphs: adjoint CG and feature gradient as two
+                                    * launches instead of the fused one (diagnostic) */
 
 typedef struct gll_problem {
     int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */
@@ -166,7 +168,9 @@ int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const f
 #define GLL_K_CG 3        /* cg_*_kernel: Jacobi-CG solves (forward and adjoint) */
 #define GLL_K_EDGE 4      /* edge_coef_kernel: auto-eps edge coefficients */
 #define GLL_K_GRAD 5      /* grad_spmm_kernel: feature gradient */
-#define GLL_K_COUNT 6
+#define GLL_K_BWD 6       /* cg_grad_fused_kernel: adjoint CG + feature gradient in one launch
+                           * (single small graphs, fixed eps) */
+#define GLL_K_COUNT 7
 int gll_prof_enable(int kid, int period);
 int gll_prof_read(int kid, double* ms_total, int* count);
 const char* gll_kernel_name(int kid);

@@ -364,6 +364,25 @@ def test_batched_graphs_equal_single_calls_bitwise(cfg, eps, ydt, exact):
             assert O.rel_err(Xb.grad[g].cpu().numpy(), gx1) <= 1e-5
 
 
+@pytest.mark.parametrize("cfg,B", [("ns", 3), ("stress", 2)])
+def test_batched_auto_eps_matches_oracle(cfg, B):
+    """The batched entry with auto epsilon (the inline-copy callers' default) at NS and at the
+    stress shape: every graph's U and grad_X against the float64 oracle on the GPU's own kNN
+    lists, forward and adjoint (GLL.py:14-177)."""
+    from graphlearninglayer_amd.synth import seeded_gbar
+    GLL = _gll()
+    Xs, Ys, c = _synth_batch(cfg, B, seed0=21)
+    G = np.stack([seeded_gbar(c["batch"], 10, 300 + g) for g in range(B)])
+    Xb = torch.from_numpy(Xs).cuda().requires_grad_(True)
+    Ub = GLL.LaplaceLearningSparseHard.apply(Xb, torch.from_numpy(Ys).cuda(), 0.07, "auto", c["k"])
+    Ub.backward(torch.from_numpy(G).cuda())
+    for g in range(B):
+        ind = _gpu_knn(Xs[g], c["k"], "auto")["knn_idx"].cpu().numpy().astype(np.int64)
+        Uo, st = O.forward(Xs[g], Ys[g], tau=0.07, epsilon="auto", K=c["k"], knn=(ind, None))
+        assert O.rel_err(Ub[g].detach().cpu().numpy(), Uo) <= TOL
+        assert O.rel_err(Xb.grad[g].cpu().numpy(), O.backward(st, G[g])) <= TOL
+
+
 def test_batched_duplicates_match_single_calls():
     """Batched selection (x_i staged in LDS, 6 waves per SIMD) on graphs with > 64 tied
     candidates, where the exact merge runs: each graph's kNN, U and grad_X agree with its
@@ -786,3 +805,86 @@ def test_presplit_gram_matches_inline_split(d):
     assert O.rel_err(Ub[0], Ui) <= 1e-5
     U2, _, _ = _forward_c_abi(X2, one_hot(lab2[:base]), k, 0.07, "auto")
     assert O.rel_err(Ub[1], U2) <= 1e-5
+
+
+def _fwd_bwd_c_abi(X, Y, k, tau, eps, gbar, flags=0, backward_calls=1):
+    """gll_forward then `backward_calls` x gll_backward on ONE workspace through ctypes."""
+    import ctypes as ct
+    from graphlearninglayer_amd import _lib
+    GLL = _gll()
+    n, d = X.shape
+    base, C = Y.shape
+    prob = GLL.make_problem(n, d, base, C, k, tau, eps, flags=flags)
+    lib = _lib.lib()
+    ws = torch.empty(lib.gll_workspace_bytes(ct.byref(prob)), dtype=torch.uint8, device="cuda")
+    U = torch.empty(n - base, C, dtype=torch.float64, device="cuda")
+    Xd = torch.from_numpy(np.ascontiguousarray(X)).cuda()
+    Yd = torch.from_numpy(np.ascontiguousarray(Y)).cuda()
+    Gd = torch.from_numpy(np.ascontiguousarray(gbar)).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.check(lib.gll_forward(ct.byref(prob), Xd.data_ptr(), Yd.data_ptr(), _lib.GLL_DT_F32,
+                               ws.data_ptr(), U.data_ptr(), s), "gll_forward")
+    grads = []
+    for _ in range(backward_calls):
+        gx = torch.empty(n, d, dtype=torch.float32, device="cuda")
+        _lib.check(lib.gll_backward(ct.byref(prob), Xd.data_ptr(), None, 0, ws.data_ptr(),
+                                    Gd.data_ptr(), _lib.GLL_DT_F64, gx.data_ptr(), s),
+                   "gll_backward")
+        grads.append(gx.cpu().numpy())
+    st = ws[: 4 * _lib.ST_NWORDS].view(torch.int32).cpu().tolist()
+    return U.cpu().numpy(), grads, st
+
+
+@pytest.mark.parametrize("cfg", ["plumbing", "ns"])
+def test_fused_backward_equals_two_launches_bitwise(cfg):
+    """The fused backward (adjoint CG + feature gradient in one launch, solve.hip
+    cg_grad_fused_kernel: single small graphs, fixed eps) against the same two kernels as two
+    launches (GLL_FLAG_BWD_UNFUSED): bitwise equal, and equal again on a second backward over
+    the same workspace (the hand-off counters re-arm); against the float64 oracle at 1e-4."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth
+    c = CONFIGS[cfg]
+    X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=6)
+    Y = one_hot(lab[: c["base"]])
+    g = seeded_gbar(c["batch"], 10, 17)
+    Uf, gf, stf = _fwd_bwd_c_abi(X, Y, c["k"], 0.07, 1.0, g, backward_calls=3)
+    Uu, gu, stu = _fwd_bwd_c_abi(X, Y, c["k"], 0.07, 1.0, g, flags=_lib.FLAG_BWD_UNFUSED)
+    np.testing.assert_array_equal(Uf, Uu)
+    for gx in gf:
+        np.testing.assert_array_equal(gx, gu[0])
+    assert stf[_lib.ST_SOLVE_FAILED] == 0 and stf[_lib.ST_BWD_NONCONV] == 0
+    assert stf[_lib.ST_BWD_ITERS] == stu[_lib.ST_BWD_ITERS] > 0
+    ind = _gpu_knn(X, c["k"], 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, st = O.forward(X, Y, tau=0.07, epsilon=1.0, K=c["k"], knn=(ind, None))
+    assert O.rel_err(gf[0], O.backward(st, g)) <= TOL
+
+
+@pytest.mark.parametrize("cfg,B,n_extra,d", [("ns", 3, 0, None), ("fullysup", 2, 0, None),
+                                             ("ns", 2, 37, 100)])
+def test_gram_256_tiles_match_128_tiles(cfg, B, n_extra, d, monkeypatch):
+    """The 256-tile pre-split Gram (knn.hip gram_pk2_kernel, 8 waves) against the 128-tile one
+    (gram_pk_kernel) on batches, ragged n and d included: the same k order and epilogue, so U
+    and grad_X agree bitwise (GLL_GRAM_TILE forces either)."""
+    from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth
+    GLL = _gll()
+    c = dict(CONFIGS[cfg])
+    if d is not None:
+        c["d"] = d
+    Xs, Ys = [], []
+    for g in range(B):
+        X, lab = synth(c["base"], c["batch"] + n_extra, c["d"], r=c["r"], seed=40 + g)
+        Xs.append(X)
+        Ys.append(one_hot(lab[: c["base"]]))
+    G = torch.from_numpy(np.stack([seeded_gbar(c["batch"] + n_extra, 10, 50 + g)
+                                   for g in range(B)])).cuda()
+    outs = []
+    for tile in ("128", "256"):
+        monkeypatch.setenv("GLL_GRAM_TILE", tile)
+        Xb = torch.from_numpy(np.stack(Xs)).cuda().requires_grad_(True)
+        U = GLL.LaplaceLearningSparseHard.apply(Xb, torch.from_numpy(np.stack(Ys)).cuda(), 0.07,
+                                                1.0, c["k"])
+        U.backward(G)
+        outs.append((U.detach().cpu().numpy(), Xb.grad.cpu().numpy()))
+    monkeypatch.delenv("GLL_GRAM_TILE")
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
