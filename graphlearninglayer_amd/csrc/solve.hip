@@ -1139,7 +1139,7 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
                                                            const float* __restrict__ X,
                                                            float* __restrict__ out,
                                                            unsigned* fsync, int32_t* st_failed,
-                                                           int poll_sleep) {
+                                                           int poll_sleep, int pre_delay) {
     const int C = c.C;
     if (int(blockIdx.x) < C) {
         cg_ell_body<NT, 1, S, TB, 1>(int2{int(blockIdx.x), 0}, fsync, c.m, C, c.base,
@@ -1149,7 +1149,9 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
                                      c.ell_w, 0, 0, 0, 0);
         return;
     }
-    // ---- gradient role: one wave per row (C = 10 classes, fixed eps)
+    // ---- gradient role: one wave per row (C = 10 classes, fixed eps).  Its ~26 MB of
+    // prefetch (x_j rows) would land on top of the solves' cold prologue loads: wait first
+    for (int q = 0; q < pre_delay; ++q) __builtin_amdgcn_s_sleep(32);
     constexpr int NC = 10;
     constexpr int EB = ND <= 2 ? 16 : 8;   // grad_spmm_kernel's single-graph (WIDE) batch
     __shared__ int s_ok;
@@ -1204,6 +1206,10 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
     float we, pj[NC];
     edge_pre(beg + lane, cj, we, pj);
     const int cnt0 = min(kWave, end - beg);
+#ifdef GLL_TRACE
+    const bool tr = int(blockIdx.x) == C && threadIdx.x == 0;   // the first gradient block
+    if (tr) g_trace[16] = __builtin_amdgcn_s_memrealtime();
+#endif
     f32x4 v[EB][ND];
 #pragma unroll
     for (int u = 0; u < EB; ++u) {
@@ -1230,6 +1236,9 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
     }
     __syncthreads();
     const bool ok = s_ok != 0;
+#ifdef GLL_TRACE
+    if (tr) g_trace[17] = __builtin_amdgcn_s_memrealtime();
+#endif
 #pragma unroll
     for (int q = 0; q < NC; ++q)
         wi[q] = __builtin_bit_cast(
@@ -1275,6 +1284,10 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
         }
     }
     __syncthreads();
+#ifdef GLL_TRACE
+    if (tr) g_trace[18] = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) atomicMax(&g_trace[19], __builtin_amdgcn_s_memrealtime());
+#endif
     if (threadIdx.x == 0) {   // the last gradient workgroup re-arms the counters
         const unsigned ng = gridDim.x - unsigned(C);
         const unsigned old = __hip_atomic_fetch_add(fsync + 32, 1u, __ATOMIC_RELAXED,
@@ -1333,8 +1346,10 @@ static hipError_t run_fused(const Layout& L, void* ws, const TB* b, const float*
     prof_begin(GLL_K_BWD, s);
     const char* ps = getenv("GLL_FUSED_SLEEP");   // diagnostic A/B of the poll interval
     const int poll_sleep = ps ? atoi(ps) : 4;
+    const char* pd = getenv("GLL_FUSED_DELAY");   // diagnostic A/B of the prefetch delay
+    const int pre_delay = pd ? atoi(pd) : 0;
     launch_k(fn, dim3(unsigned(G)), NT, lds, s, c, a, X, gradX, L.at<unsigned>(ws, L.fsync),
-             st_failed, poll_sleep);
+             st_failed, poll_sleep, pre_delay);
     prof_end(GLL_K_BWD, s);
     return launch_status("solve.hip:run_fused");
 }

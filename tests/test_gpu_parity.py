@@ -807,7 +807,7 @@ def test_presplit_gram_matches_inline_split(d):
     assert O.rel_err(Ub[1], U2) <= 1e-5
 
 
-def _fwd_bwd_c_abi(X, Y, k, tau, eps, gbar, flags=0, backward_calls=1):
+def _fwd_bwds_c_abi(X, Y, k, tau, eps, gbar, flags=0, backward_calls=1):
     """gll_forward then `backward_calls` x gll_backward on ONE workspace through ctypes."""
     import ctypes as ct
     from graphlearninglayer_amd import _lib
@@ -847,8 +847,8 @@ def test_fused_backward_equals_two_launches_bitwise(cfg):
     X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=6)
     Y = one_hot(lab[: c["base"]])
     g = seeded_gbar(c["batch"], 10, 17)
-    Uf, gf, stf = _fwd_bwd_c_abi(X, Y, c["k"], 0.07, 1.0, g, backward_calls=3)
-    Uu, gu, stu = _fwd_bwd_c_abi(X, Y, c["k"], 0.07, 1.0, g, flags=_lib.FLAG_BWD_UNFUSED)
+    Uf, gf, stf = _fwd_bwds_c_abi(X, Y, c["k"], 0.07, 1.0, g, backward_calls=3)
+    Uu, gu, stu = _fwd_bwds_c_abi(X, Y, c["k"], 0.07, 1.0, g, flags=_lib.FLAG_BWD_UNFUSED)
     np.testing.assert_array_equal(Uf, Uu)
     for gx in gf:
         np.testing.assert_array_equal(gx, gu[0])

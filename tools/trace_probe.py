@@ -105,6 +105,13 @@ def timeline(tr, label):
         print("cg block 0 wave 0, iteration 3 (shader cycles): " +
               ", ".join(f"{lab[q]} {cyc[q + 1] - cyc[q]}" for q in range(5)) +
               f" | total {cyc[5] - cyc[0]}")
+    fz = tr[2].astype(np.int64)
+    if fz[16] and fz[32] and fz[32] < 2 ** 62:
+        base = fz[32]   # first entry of the solve kernel (the CG role of the fused backward)
+        print("fused backward (us from the first CG entry): " + ", ".join(
+            f"{nm} +{TICK_US * (fz[q] - base):.2f}" for q, nm in
+            [(16, "grad block C prefetch issued"), (17, "its wait over"), (18, "its rows stored"),
+             (33, "last CG exit"), (19, "last grad exit")] if fz[q]))
     pts = tr[2][:10].astype(np.int64)
     if pts[0]:
         print("cg block 0: " + ", ".join(f"{CG_PTS[i]} +{TICK_US * (pts[i] - pts[0]):.2f}"
