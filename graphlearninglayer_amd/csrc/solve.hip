@@ -1081,12 +1081,15 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
     // request would pin one per CU); a single graph's C workgroups take all the LDS there is
     // (K = 25 rows overflow 16 slots by ~14K entries at m = 1250)
     const int64_t kOvfLds = bt.B == 1 ? int64_t(1) << 30 : 2048;
+    static const char* pad_env = getenv("GLL_CG_LDS_PAD");   // diagnostic: bytes of LDS per
+    const size_t lds_pad = pad_env ? size_t(atoi(pad_env)) : 0;   // workgroup at least
     const int64_t eu_bound = int64_t(L.m + L.n) * (L.K - 1);
     int64_t cap = int64_t(kLdsDyn - lds) / 8;
     if (cap > eu_bound) cap = eu_bound;
     if (cap > kOvfLds) cap = kOvfLds;
     if (cap < 0) cap = 0;
     lds += size_t(cap) * 8;
+    if (lds < lds_pad) lds = lds_pad;
     if (S != ell_emit(L, bt.B)) {   // row_build emitted ell_emit(L, B) slots
         (void)hipGetLastError();
         if (getenv("GLL_DEBUG"))
