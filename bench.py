@@ -97,7 +97,17 @@ def launch(a) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps):
+def cg_spmvs(iters, B, m):
+    """Matrix passes (SpMVs) of one CG solve of `iters` iterations, by the solver the library
+    picks (solve.hip cg_dispatch): the register-ELL kernel with one row per thread (single
+    graphs with m <= 512, batches with m <= 256) runs the Neumann-preconditioned form, two
+    passes per iteration plus two in setup; every other per-column kernel one per iteration
+    plus the pre-step."""
+    neumann = m <= 512 and (B == 1 or m <= 256)
+    return 2 * iters + 2 if neumann else iters + 1
+
+
+def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps, B=1):
     """Algorithmic work per launch of each kernel (SURVEY.md §8d byte/flop model)."""
     n, d, K, m, C = cfg["n"], cfg["d"], cfg["k"], cfg["batch"], 10
     E, nnz_uu = graph_stats
@@ -106,26 +116,28 @@ def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps):
         "gram_d2_kernel": ("mfma", 2.0 * n * n * d),
         "knn_select_kernel": ("hbm", 4.0 * n * n + 8.0 * n * K),
         "row_build_kernel": ("hbm", 16.0 * E + 8.0 * n * K + 4 * n + 4 * m * C),
-        # SURVEY §8d SpMV roofline: B_spmv per iteration (the matrix and one gathered vector);
-        # the call roofline prices a whole CG iteration instead (cg_iteration_bytes)
-        "cg_kernel": ("hbm", 0.5 * (iters_fwd + iters_bwd) * b_spmv),
+        # SURVEY §8d SpMV roofline: B_spmv per matrix pass (the matrix and one gathered
+        # vector), times the passes the solve made; the call roofline prices a whole CG
+        # iteration instead (cg_iteration_bytes)
+        "cg_kernel": ("hbm", 0.5 * (cg_spmvs(iters_fwd, B, m) + cg_spmvs(iters_bwd, B, m)) * b_spmv),
         "edge_coef_kernel": ("hbm", 16.0 * E + 8.0 * n * C),
         "grad_spmm_kernel": ("hbm", (12.0 * E + 8.0 * n * d) if auto_eps
                              else (8.0 * E + 8.0 * n * C + 8.0 * n * d)),
     }
     # the fused backward of a single small graph (adjoint CG + feature gradient, one launch)
-    u["cg_grad_fused_kernel"] = ("hbm", iters_bwd * b_spmv + u["grad_spmm_kernel"][1])
+    u["cg_grad_fused_kernel"] = ("hbm", cg_spmvs(iters_bwd, B, m) * b_spmv + u["grad_spmm_kernel"][1])
     return u
 
 
-def cg_iteration_bytes(cfg, graph_stats, iters_fwd, iters_bwd):
+def cg_iteration_bytes(cfg, graph_stats, iters_fwd, iters_bwd, B=1):
     """§8d's whole CG iteration, B_spmv + 28 mC: the SpMV plus the vector updates (x, r, p, z
     read/written once each), which this library keeps in registers and LDS -- an 'effective'
-    figure, reported beside the SpMV roofline and used by the call roofline."""
+    figure, reported beside the SpMV roofline and used by the call roofline.  Matrix passes
+    as the solver makes them (cg_spmvs)."""
     m, C = cfg["batch"], 10
     _, nnz_uu = graph_stats
     b_spmv = 8 * nnz_uu + 8 * m + 8 * m * C
-    return 0.5 * (iters_fwd + iters_bwd) * (b_spmv + 28 * m * C)
+    return 0.5 * sum(cg_spmvs(it, B, m) * b_spmv + it * 28 * m * C for it in (iters_fwd, iters_bwd))
 
 
 def cg_roofline_extras(work_spmv, work_iter, avg_s, traffic):
@@ -199,7 +211,7 @@ def gram_mfma_pmc(config):
     return None
 
 
-def batched_measure(c, eps, tau, k, B, units, cg_iter_work, dev, rank, steps=20, warmup=5):
+def batched_measure(c, eps, tau, k, B, gstats, dev, rank, steps=20, warmup=5):
     """B independent graphs of the workload per call of the batched entry point (X: B x n x d):
     whole-batch fwd+bwd throughput, and the CG kernel against the HBM roofline, where one
     launch now carries B graphs' SpMVs ('reported at batched NS')."""
@@ -219,6 +231,10 @@ def batched_measure(c, eps, tau, k, B, units, cg_iter_work, dev, rank, steps=20,
         U = lap(Xb, Yb, tau, eps, k)
         return torch.autograd.grad(U, Xb, G)
 
+    # the batched launches' own CG iterations (their solver differs from the single graph's)
+    it_f, it_b = _cg_iters(Xb, Yb, tau, eps, k, G)
+    units = kernel_units(c, gstats, it_f, it_b, isinstance(eps, str), B=B)
+    cg_iter_work = cg_iteration_bytes(c, gstats, it_f, it_b, B=B)
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -248,7 +264,7 @@ def batched_measure(c, eps, tau, k, B, units, cg_iter_work, dev, rank, steps=20,
             "ms_per_step": round(1e3 * elapsed / steps, 4),
             "note": "one fwd+bwd of the batched entry point = B graphs; every CG launch "
                     "timed by events carried in its dispatch packet",
-            "roofline": roof,
+            "roofline": roof, "cg_iters_fwd_bwd": [it_f, it_b],
             "gram_mfma_pmc": gram_mfma_pmc(f"{c['name']}_b{B}")}
 
 
@@ -539,6 +555,18 @@ def main():
                                       "time / 8 TB/s, B_spmv = 8 nnz_off(Luu) + 8 m + 8 m C")
             roofline["spmv_frac"] = roofline["frac"]
             roofline.update(cg_roofline_extras(work, cg_iter_work, avg_s, traffic))
+        # SURVEY §8d's SpMV roofline of the forward CG launch (reported whatever kernel dominates;
+        # the backward's CG may run inside the fused backward launch)
+        if "cg_kernel" in per_kernel:
+            t_cg = per_kernel["cg_kernel"]["us_per_launch"] * 1e-6
+            w_cg = units["cg_kernel"][1]
+            roofline["sec8d_cg_spmv"] = {
+                "kernel": "cg_kernel", "work_per_launch": w_cg, "us_per_launch": round(t_cg * 1e6, 3),
+                "achieved_GBs": round(w_cg / t_cg / 1e9, 3),
+                "frac": round(w_cg / t_cg / 1e9 / HBM_PEAK_GBS, 5),
+                "note": "B_spmv x iterations / launch time / 8 TB/s; a single NS graph is "
+                        "latency-bound (SURVEY §7: 30% would need 29 ns per SpMV) -- the batched "
+                        "line below carries the meaningful SpMV figure"}
         # whole-call roofline: kNN at its MFMA roof + every other byte at HBM,
         # a CG priced per whole iteration (B_spmv + 28 mC)
         f_knn = units["gram_d2_kernel"][1]
@@ -560,7 +588,7 @@ def main():
 
     batched = None
     if a.batch > 0 and roofline is not None:
-        batched = batched_measure(c, eps, tau, k, a.batch, units, cg_iter_work, dev, rank)
+        batched = batched_measure(c, eps, tau, k, a.batch, gstats, dev, rank)
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
@@ -618,24 +646,28 @@ def main():
 
 
 def _cg_iters(X, Y, tau, eps, k, gbar):
-    """CG iterations (max over columns) of one fwd and one bwd solve on the bench input."""
+    """CG iterations (max over columns) of one fwd and one bwd solve on the bench input
+    (X: n x d, or B x n x d through the batched entry points: graph 0's solves)."""
     import ctypes as ct
 
-    n, d = X.shape
-    base, C = Y.shape
+    B = X.shape[0] if X.dim() == 3 else 1
+    n, d = X.shape[-2:]
+    base, C = Y.shape[-2:]
     prob = GLL.make_problem(n, d, base, C, k, tau, eps)
     lib = _lib.lib()
-    ws = torch.empty(lib.gll_workspace_bytes(ct.byref(prob)), dtype=torch.uint8, device=X.device)
-    U = torch.empty(n - base, C, dtype=torch.float64, device=X.device)
+    nb = lib.gll_workspace_bytes(ct.byref(prob))
+    ws = torch.empty(nb * B, dtype=torch.uint8, device=X.device)
+    U = torch.empty(B, n - base, C, dtype=torch.float64, device=X.device)
     X32 = X.detach().contiguous()
     Yc = Y.contiguous()
     s = torch.cuda.current_stream(X.device).cuda_stream
-    _lib.check(lib.gll_forward(ct.byref(prob), X32.data_ptr(), Yc.data_ptr(), _lib.GLL_DT_F32,
-                               ws.data_ptr(), U.data_ptr(), s), "gll_forward")
-    gx = torch.empty(n, d, dtype=torch.float32, device=X.device)
-    _lib.check(lib.gll_backward(ct.byref(prob), X32.data_ptr(), None, 0, ws.data_ptr(),
-                                gbar.data_ptr(), _lib.GLL_DT_F64, gx.data_ptr(), s),
-               "gll_backward")
+    _lib.check(lib.gll_forward_batched(ct.byref(prob), B, X32.data_ptr(), Yc.data_ptr(),
+                                       _lib.GLL_DT_F32, ws.data_ptr(), U.data_ptr(), s),
+               "gll_forward")
+    gx = torch.empty(B, n, d, dtype=torch.float32, device=X.device)
+    _lib.check(lib.gll_backward_batched(ct.byref(prob), B, X32.data_ptr(), ws.data_ptr(),
+                                        gbar.contiguous().data_ptr(), _lib.GLL_DT_F64,
+                                        gx.data_ptr(), s), "gll_backward")
     st = ws[: 4 * _lib.ST_NWORDS].view(torch.int32).cpu().tolist()
     return st[_lib.ST_FWD_ITERS], st[_lib.ST_BWD_ITERS]
 

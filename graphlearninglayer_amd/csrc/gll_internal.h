@@ -220,17 +220,13 @@ struct Layout {
     T* at(void* ws, size_t o) const { return reinterpret_cast<T*>(static_cast<char*>(ws) + o); }
 };
 
-// ELL slots row_build writes and the per-column CG reads for a launch over B graphs.  The
-// region holds L.SE (24 for m <= 512); batched launches use the first 12: at NS a U row holds
-// 6.4 entries on average (3.6% of rows past 12, 69 entries a graph, which go to the LDS
-// overflow), and the prologue of a B = 64 launch spent 10 of its 28 us loading 24 slots per
-// row in each of the C column workgroups (trace build).  GLL_CG_BS = 8 / 16 / 24 (diagnostic)
-// overrides.
+// ELL slots row_build writes and the per-column CG reads for a launch over B graphs: the
+// region's L.SE.  (Round 3 measured narrower slices for batches -- 12 or 16 of the 24 slots,
+// the longer rows' tails in the LDS overflow -- and dropped them: B = 64 NS CG 21.6 us at 24
+// slots against 26.9 at 16 and 29.6 at 12, profiles/r03j_batched_ell_width_ab.txt.)
 inline int ell_emit(const Layout& L, int B) {
-    if (B <= 1 || L.SE != 24 || (L.flags & (GLL_FLAG_CG_CLASSIC | GLL_FLAG_CG_PIPE))) return L.SE;
-    const char* e = getenv("GLL_CG_BS");
-    const int v = e ? atoi(e) : 12;
-    return (v == 8 || v == 16 || v == 24) ? v : 12;
+    (void)B;
+    return L.SE;
 }
 
 // Planes the Gram kernel of a launch over B graphs writes (= planes the select kernel sums).

@@ -190,7 +190,8 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int& total) 
     }
 }
 
-// MODE: 0 classic PCG (two reductions), 1 Chronopoulos-Gear (one reduction, two barriers),
+// MODE: 3 Chronopoulos-Gear with a first-order Neumann preconditioner (below; the default),
+// 0 classic PCG (two reductions), 1 Chronopoulos-Gear (one reduction, two barriers),
 // 2 pipelined PCG (Ghysels-Vanroose: one barrier per iteration).
 // The kernel body: `gxy` = (column, graph); `fsync` (the fused backward, cg_grad_fused_kernel)
 // non-null: the solution is stored write-through (sc1) and, once every wave has drained its
@@ -227,7 +228,7 @@ __device__ __forceinline__ void cg_ell_body(
     int* scan = reinterpret_cast<int*>(smem + 96);      // 16 ints of scan scratch
     const int mp4 = (m + 3) & ~3;
     float* P_ = smem + 128;                             // gathered vector (x2 when pipelined)
-    int* lcol = reinterpret_cast<int*>(P_ + (MODE == 2 ? 2 : 1) * mp4);   // overflow, compacted
+    int* lcol = reinterpret_cast<int*>(P_ + (MODE >= 2 ? 2 : 1) * mp4);   // overflow, compacted
     float* lw = reinterpret_cast<float*>(lcol + mat_cap);
     // (Ordering rows by length so each wave's slot bound tracks its own rows was measured:
     // no gain per iteration at NS, +1.5 us of setup from the permuted ELL loads.)
@@ -382,10 +383,36 @@ __device__ __forceinline__ void cg_ell_body(
             }
             return dg[q] * pq - acc;   // (Luu u)_row = (deg + tau) u_row - sum_j W_rowj u_j
         };
-        if constexpr (MODE == 1) {
+        if constexpr (MODE == 1 || MODE == 3) {
         // Chronopoulos-Gear single-reduction PCG: one fused (r.u, w.u, r.r) exchange and one
         // publish barrier per iteration (classic PCG: two exchanges + publish = 3 barriers).
         // s = A p by recurrence; u = M^-1 r is what is published and multiplied.
+        // MODE 3: M^-1 = D^-1 + D^-1 N D^-1 (A = D - N, N the off-diagonal weights W_uj >= 0:
+        // the first two terms of the Neumann series of A^-1), applied as y = D^-1 r published,
+        // u = y + D^-1 (N y) -- one more gather and barrier per iteration.  It is SPD where
+        // D^-1/2 A D^-1/2 has its spectrum in (0, 2), which diagonal dominance gives, and turns
+        // that spectrum [l, h] into {x (2 - x)}: at NS [0.44, 1.32] -> [0.69, 1], 11 -> 6
+        // iterations, so each iteration's fixed reduction and step-size latency is paid about
+        // half as often (tools/ab_flags.py).
+        constexpr bool NEU = MODE == 3;
+        float* P2_ = P_ + mp4;   // y = D^-1 r (MODE 3)
+        if constexpr (NEU) {
+            // setup left y0 = D^-1 r0 in P_ (as p) and rz = (r0, y0): u0 = y0 + D^-1 N y0
+            rz = 0.f;
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                const float t = -spmv(q, 0.f, P_);   // (N y0)_row
+                p[q] = p[q] + mi[q] * t;
+                rz += r[q] * p[q];
+            }
+            __syncthreads();   // every gather of y0 is done before u0 overwrites it
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                const int u = urow[q];
+                if (u < m) P_[u] = p[q];
+            }
+            __syncthreads();
+        }
         // pre-step: w0 = A u0 (u0 = p, already published), gamma0 = (r,u), delta0 = (w,u)
         float sv[R];
         float dl = 0.f;
@@ -416,9 +443,18 @@ __device__ __forceinline__ void cg_ell_body(
             for (int q = 0; q < R; ++q) {
                 x[q] += alpha * p[q];
                 r[q] -= alpha * sv[q];
-                ap[q] = mi[q] * r[q];                       // u = M^-1 r
+                ap[q] = mi[q] * r[q];                       // u = M^-1 r (MODE 3: y)
                 const int u = urow[q];
-                if (u < m) P_[u] = ap[q];
+                if (u < m) (NEU ? P2_ : P_)[u] = ap[q];
+            }
+            if constexpr (NEU) {   // u = y + D^-1 (N y)
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < R; ++q) {
+                    ap[q] += mi[q] * -spmv(q, 0.f, P2_);
+                    const int u = urow[q];
+                    if (u < m) P_[u] = ap[q];
+                }
             }
             GLL_TRACE_CYC(11);
             if constexpr (NT > kWave) __syncthreads();
@@ -1075,7 +1111,7 @@ template <int NT, int R, int S, typename TB, int MODE>
 static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* b, size_t bs,
                           double* out64, float* out32, float rtol, int max_iter,
                           int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
-    size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4 * (MODE == 2 ? 2 : 1);
+    size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4 * (MODE >= 2 ? 2 : 1);
     // entries past the ELL slices are compacted into LDS up to kOvfLds of them, the rest read
     // from the CSR; batched launches cap them so 4 workgroups still share a CU (a full-LDS
     // request would pin one per CU); a single graph's C workgroups take all the LDS there is
@@ -1145,7 +1181,7 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
                                                            int poll_sleep, int pre_delay) {
     const int C = c.C;
     if (int(blockIdx.x) < C) {
-        cg_ell_body<NT, 1, S, TB, 1>(int2{int(blockIdx.x), 0}, fsync, c.m, C, c.base,
+        cg_ell_body<NT, 1, S, TB, 3>(int2{int(blockIdx.x), 0}, fsync, c.m, C, c.base,
                                      c.row_start, c.row_len, c.ucnt, c.col, c.wv, c.diag,
                                      static_cast<const TB*>(c.b), nullptr, c.out32, c.rtol,
                                      c.max_iter, c.mat_cap, c.st_nonconv, c.st_iters, c.ell_col,
@@ -1309,7 +1345,7 @@ static hipError_t run_fused(const Layout& L, void* ws, const TB* b, const float*
                             int32_t* st_nonconv, int32_t* st_iters, int32_t* st_failed,
                             hipStream_t s) {
     constexpr int S = 24;
-    size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4;
+    size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4 * 2;   // MODE 3: P and y
     const int64_t eu_bound = int64_t(L.m + L.n) * (L.K - 1);
     int64_t cap = int64_t(kLdsDyn - lds) / 8;
     if (cap > eu_bound) cap = eu_bound;
@@ -1365,11 +1401,13 @@ hipError_t launch_cg_grad_fused(const Layout& L, void* ws, const void* gbar, int
     if (L.C != 10 || !(eps_fixed > 0.f) || !vec || m < 1 || m > 512 || L.RV != 0 ||
         ell_emit(L, 1) != 24 || L.d > 1024)
         return hipErrorNotSupported;
-    if (L.flags & (GLL_FLAG_BWD_UNFUSED | GLL_FLAG_CG_GRID | GLL_FLAG_CG_CLASSIC |
-                   GLL_FLAG_CG_PIPE | GLL_FLAG_GRAD_CHUNK))
+    const char* fe = getenv("GLL_BWD_FUSED");   // diagnostic A/B through the torch layer
+    if ((L.flags & GLL_FLAG_BWD_UNFUSED) || (fe && fe[0] == '0') ||
+        (L.flags & (GLL_FLAG_CG_GRID | GLL_FLAG_CG_CLASSIC | GLL_FLAG_CG_PIPE | GLL_FLAG_GRAD_CHUNK)))
         return hipErrorNotSupported;
     if (size_t(L.n) * L.d * 4 > (size_t(4) << 20)) return hipErrorNotSupported;   // chunked
-    if (getenv("GLL_CG_NT")) return hipErrorNotSupported;   // diagnostic CG shapes: unfused
+    if (getenv("GLL_CG_NT") || getenv("GLL_CG_MODE"))   // diagnostic CG shapes: unfused
+        return hipErrorNotSupported;
     const int nd = (L.d + 255) / 256;
 #define GLL_FUSED(NT_)                                                                       \
     {                                                                                        \
@@ -1431,6 +1469,11 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
         if (e != hipErrorNotSupported) return e;
         // no grid configuration holds it: per-column kernels below (any m)
     }
+    // the Neumann form (MODE 3) wherever a thread owns one row; batched launches with two rows
+    // per thread keep one SpMV per iteration (MODE 3 at 256 x 2 takes 220 VGPRs, two waves per
+    // SIMD instead of three: B = 64 NS CG 21.8 -> 34.2 us; profiles/r03l_cg_neumann_ab.txt).
+    // GLL_CG_MODE = 1 / 3: A/B.
+    static const int cg_mode_env = getenv("GLL_CG_MODE") ? atoi(getenv("GLL_CG_MODE")) : 0;
 #define GLL_ELL(NT, R, S)                                                                   \
     return (L.flags & GLL_FLAG_CG_CLASSIC)                                                  \
                ? run_ell<NT, R, S, TB, 0>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
@@ -1438,7 +1481,10 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
            : (L.flags & GLL_FLAG_CG_PIPE)                                                   \
                ? run_ell<NT, R, S, TB, 2>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
                                           st_nonconv, st_iters, s)                          \
-               : run_ell<NT, R, S, TB, 1>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
+           : (cg_mode_env ? cg_mode_env == 1 : (bt.B > 1 && R > 1))                          \
+               ? run_ell<NT, R, S, TB, 1>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
+                                          st_nonconv, st_iters, s)                          \
+               : run_ell<NT, R, S, TB, 3>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
                                           st_nonconv, st_iters, s)
     if (L.RV > 0) {   // the balanced kernel (row_build packed its virtual rows)
 #define GLL_VR(T_, R_, V_) \
@@ -1450,28 +1496,6 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
         GLL_VR(512, 4, 4); GLL_VR(512, 4, 8); GLL_VR(512, 4, 10);
 #undef GLL_VR
         return hipErrorInvalidValue;
-    }
-    // batched launches: the narrower ELL slice of ell_emit (same thread layout as a single
-    // call, so the sums run in the same order; single-reduction form only)
-    const int se = ell_emit(L, bt.B);
-    if (m <= 512 && se != 24) {
-#define GLL_ELLB(NT_, R_)                                                                   \
-        {                                                                                   \
-            if (se == 8)                                                                    \
-                return run_ell<NT_, R_, 8, TB, 1>(L, bt, ws, b, bs, out64, out32, rtol,     \
-                                                  max_iter, st_nonconv, st_iters, s);       \
-            if (se == 12)                                                                   \
-                return run_ell<NT_, R_, 12, TB, 1>(L, bt, ws, b, bs, out64, out32, rtol,    \
-                                                   max_iter, st_nonconv, st_iters, s);      \
-            if (se == 16)                                                                   \
-                return run_ell<NT_, R_, 16, TB, 1>(L, bt, ws, b, bs, out64, out32, rtol,    \
-                                                   max_iter, st_nonconv, st_iters, s);      \
-        }
-        if (m <= 64) GLL_ELLB(64, 1);
-        if (m <= 128) GLL_ELLB(128, 1);
-        if (m <= 256) GLL_ELLB(256, 1);
-        GLL_ELLB(256, 2);
-#undef GLL_ELLB
     }
     if (m <= 64) GLL_ELL(64, 1, 24);
     if (m <= 128) GLL_ELL(128, 1, 24);

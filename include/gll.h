@@ -72,8 +72,9 @@ extern "C" {
                                   * run (d >= 128, d % 4 == 0) (diagnostic) */
 #define GLL_FLAG_GRAM_INLINE 8192 /* 128-tile Gram: split each tile's rows inline (the round-1
                                    * kernel) instead of pre-split planes + LDS-DMA (diagnostic) */
-#define GLL_FLAG_BWD_UNFUSED 16384 /* single small graphs: adjoint CG and feature gradient as two
-                                    * launches instead of the fused one (diagnostic) */
+#define GLL_FLAG_BWD_UNFUSED 16384 /* single small graphs, fixed eps: adjoint CG and feature
+                                    * gradient as two launches instead of the fused one
+                                    * (diagnostic) */
 
 typedef struct gll_problem {
     int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */

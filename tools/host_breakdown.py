@@ -105,3 +105,14 @@ timeit("step: apply + autograd.grad", step)
 timeit("step: apply + U.backward", step_bwd)
 timeit("torch op x.add_(1)", tiny)
 timeit("autograd.grad(a*2)", tiny_grad)
+with torch.autograd.set_multithreading_enabled(False):
+    timeit("step, autograd single-threaded", step)
+    timeit("autograd.grad(a*2), single-threaded", tiny_grad)
+
+
+def launch_only():   # one trivial HIP kernel through the C ABI's cheapest entry (status probe)
+    lib.gll_backward(ct.byref(prob), Xd.data_ptr(), None, 0, ws.data_ptr(), g.data_ptr(),
+                     _lib.GLL_DT_F64, gx.data_ptr(), s)
+
+
+timeit("raw C-ABI bwd (2 launches)", launch_only)
