@@ -10,7 +10,7 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgll.so")
+LIB_PATH = os.environ.get("GLL_LIB_PATH") or os.path.join(HERE, "libgll.so")  # env: A/B builds
 
 GLL_OK = 0
 GLL_DT_F32, GLL_DT_F64, GLL_DT_I64 = 0, 1, 2

@@ -1034,6 +1034,161 @@ __device__ __forceinline__ bool merge_threshold(const uint64_t (&key)[KS], int k
     return redo;
 }
 
+// Threshold scan (round 3; replaces scan_row + merge_threshold for kc <= 32): each lane keeps
+// only its TOP smallest D2 bits (min/max network, ~2 VALU per slot, against the ~35 of a sorted
+// 64-bit list insert: the batched select was VALU-issue bound), T = the kc-th smallest of the
+// 64 x TOP lane entries by bisection -- at least kc distinct columns are <= T, so the kc-th
+// smallest D2 is too -- and every column with D2 bits <= T is compacted into the wave's LDS
+// slots in column order.  Simulated at kc = 13 / n = 1,000 (TOP = 2) the set averages 13.2
+// columns, at kc = 32 / n = 1,500 (TOP = 3) 32.4.  CH > 0: the row (n <= 1024 CH) stays in
+// registers between the two passes; CH = 0 re-reads it (L1/L2-hot).  Returns true when more
+// than 64 columns tie in (the caller re-runs the exact merge).  tb: D2 bits every left-out
+// column is >= to (+inf when every valid column is a candidate).
+constexpr int kSelNB = 4;   // float4 per lane per 1024-column chunk of a D2 row
+
+// Loads of CH 1024-column chunks of D2 row `row` (sum of NP planes), clamped past ld.
+template <int NP, int CH>
+__device__ __forceinline__ void load_d2_row(const float* __restrict__ row, size_t plane, int ld,
+                                            f32x4 (&v)[CH * kSelNB]) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int b = 0; b < kSelNB; ++b) {
+            const int j0 = c * 4 * kWave * kSelNB + 4 * (b * kWave + lane);
+            const int jc = j0 < ld ? j0 : 0;
+            v[c * kSelNB + b] = *reinterpret_cast<const f32x4*>(row + jc);
+#pragma unroll
+            for (int p = 1; p < NP; ++p)
+                v[c * kSelNB + b] += *reinterpret_cast<const f32x4*>(row + p * plane + jc);
+        }
+}
+
+template <int TOP, int NP, int CH>
+__device__ __forceinline__ bool select_threshold(const float* __restrict__ row, size_t plane,
+                                                 int n, int ld, int i, int kc,
+                                                 int* __restrict__ cand,
+                                                 uint32_t* __restrict__ cgd, int& ci, int& kce,
+                                                 uint32_t& tb, uint32_t& gbits,
+                                                 const f32x4 (&vin)[CH > 0 ? CH * kSelNB : 1]) {
+    constexpr int NB = kSelNB;
+    constexpr int HV = CH > 0 ? CH * NB * 4 : 1;
+    const int lane = lane_id();
+    uint32_t m[TOP];
+#pragma unroll
+    for (int t = 0; t < TOP; ++t) m[t] = 0xFFFFFFFFu;
+    uint32_t hv[HV];
+    auto load_chunk = [&](int jb, f32x4 (&v)[NB]) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int j0 = jb + 4 * (b * kWave + lane);
+            const int jc = j0 < ld ? j0 : 0;
+            v[b] = *reinterpret_cast<const f32x4*>(row + jc);
+#pragma unroll
+            for (int p = 1; p < NP; ++p) v[b] += *reinterpret_cast<const f32x4*>(row + p * plane + jc);
+        }
+    };
+    auto bits_of = [&](float x, int j) -> uint32_t {   // invalid: 0xFFFFFFFF (> any T)
+        return (j < n && j != i && x == x) ? __float_as_uint(x > 0.f ? x : 0.f) : 0xFFFFFFFFu;
+    };
+    int nvalid = 0;
+    // pass 1: per-lane TOP smallest
+    auto absorb = [&](uint32_t u) {
+        nvalid += u != 0xFFFFFFFFu ? 1 : 0;
+#pragma unroll
+        for (int t = 0; t < TOP; ++t) {
+            const uint32_t lo = m[t] < u ? m[t] : u;
+            u = m[t] < u ? u : m[t];
+            m[t] = lo;
+        }
+    };
+    if constexpr (CH > 0) {   // the row was loaded by the caller (prefetched under the last row)
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint32_t u = bits_of(vin[c * NB + b][t], c * 4 * kWave * NB + 4 * (b * kWave + lane) + t);
+                    hv[(c * NB + b) * 4 + t] = u;
+                    absorb(u);
+                }
+        }
+    } else {
+        for (int jb = 0; jb < n; jb += 4 * kWave * NB) {
+            f32x4 v[NB];
+            load_chunk(jb, v);
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) absorb(bits_of(v[b][t], jb + 4 * (b * kWave + lane) + t));
+        }
+    }
+    GLL_TRACE_PT(16);
+    auto count_le = [&](uint32_t t) {
+        int c = 0;
+#pragma unroll
+        for (int s = 0; s < TOP; ++s) c += __popcll(__ballot(m[s] <= t));
+        return c;
+    };
+    uint32_t T = 0xFFFFFFFEu;   // fewer than kc valid entries: every valid column
+    if (count_le(T) >= kc) {
+        // between the smallest entry and the largest valid one
+        uint32_t top = 0;
+#pragma unroll
+        for (int s = 0; s < TOP; ++s) top = m[s] != 0xFFFFFFFFu ? m[s] : top;
+        uint32_t lo = wave_min_u32(m[0]), up = wave_max_u32(top);
+        while (lo < up) {   // smallest T with count_le(T) >= kc (wave-uniform, <= 32 steps)
+            const uint32_t mid = lo + ((up - lo) >> 1);
+            if (count_le(mid) >= kc) up = mid;
+            else lo = mid + 1u;
+        }
+        T = up;
+    }
+    // pass 2: compact every column <= T, in column order
+    int base = 0, mine = 0;
+    auto emit = [&](uint32_t u, int j) {
+        const bool p = u <= T;
+        const uint64_t mk = __ballot(p);
+        const int pos = base + lanes_below(mk);
+        if (p && pos < kWave) {
+            cand[pos] = j;
+            cgd[pos] = u;
+        }
+        mine += p ? 1 : 0;
+        base += __popcll(mk);
+    };
+    if constexpr (CH > 0) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    emit(hv[(c * NB + b) * 4 + t], c * 4 * kWave * NB + 4 * (b * kWave + lane) + t);
+    } else {
+        for (int jb = 0; jb < n; jb += 4 * kWave * NB) {
+            f32x4 v[NB];
+            load_chunk(jb, v);
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int j = jb + 4 * (b * kWave + lane) + t;
+                    emit(bits_of(v[b][t], j), j);
+                }
+        }
+    }
+    const bool redo = base > kWave;
+    tb = __ballot(mine != nvalid) == 0 ? 0x7F800000u : T + 1u;
+    __builtin_amdgcn_wave_barrier();   // a wave's LDS ops run in order: the reads see the stores
+    asm volatile("" ::: "memory");
+    kce = base;
+    ci = (!redo && lane < base) ? cand[lane] : -1;
+    gbits = (!redo && lane < base) ? cgd[lane] : 0xFFFFFFFFu;
+    return redo;
+}
+
 // 64-bit DPP add of the 8-lane group butterfly (two 32-bit moves per stage).
 template <int CTRL>
 __device__ __forceinline__ double dpp_add_d(double v) {
@@ -1231,16 +1386,20 @@ __device__ __forceinline__ KnnPick knn_rescan(const float* __restrict__ row, siz
     return KnnPick{bd, bi};
 }
 
-// XQ > 0: x_i staged in LDS, d <= 256 XQ
-template <int KC, bool VEC, int NP, int PG, int NU, int XQ = 0, bool R = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XQ > 0 && NU <= 8 ? 6 : 1)))
+// XQ > 0: x_i staged in LDS, d <= 256 XQ.  CH > 0 (KC <= 32): n <= 1024 CH, the D2 row held in
+// registers by the threshold scan.
+template <int KC, bool VEC, int NP, int PG, int NU, int XQ = 0, bool R = false, int CH = 0>
+#ifndef GLL_SEL_WAVES
+#define GLL_SEL_WAVES 6
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XQ > 0 && NU <= 8 ? GLL_SEL_WAVES : 1)))
 void knn_select_kernel(
     const float* __restrict__ D2, int ld, size_t plane, const float* __restrict__ X, int n, int d, int K,
     int kc, float eps_fixed, int auto_eps, int RCAP, int32_t* __restrict__ knn_idx,
     float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ rev_cnt,
     int32_t* __restrict__ rev_idx, float* __restrict__ rev_d2, int32_t* __restrict__ ovf,
     int32_t* __restrict__ status, int32_t* __restrict__ status_pub, size_t xs, size_t wss,
-    size_t sts) {
+    size_t sts, int diag) {
     GLL_TRACE_SCOPE(1);
     GLL_TRACE_PT(20);
     const int2 gxy = batch_xy<R>();   // once (per pointer it re-reads gridDim and divides)
@@ -1283,15 +1442,28 @@ void knn_select_kernel(
     int ci, kce;
     uint32_t tb, gb;   // gb: this lane's candidate's Gram D2 bits
     {
-        uint64_t key[KS];
-        const int seen = scan_row<KS, NP>(row, plane, n, ld, i, key);
-        GLL_TRACE_PT(16);
-        if constexpr (XL) {
+        bool redo;
+        if constexpr (KC <= 32) {
+            f32x4 vrow[CH > 0 ? CH * kSelNB : 1];
+            if constexpr (CH > 0) load_d2_row<NP, CH>(row, plane, ld, vrow);
+            redo = select_threshold<KC == 16 ? 2 : 3, NP, CH>(row, plane, n, ld, i, kc, s_cand[wv],
+                                                              s_cgd[wv], ci, kce, tb, gb, vrow);
+            if constexpr (XL) {
 #pragma unroll
-            for (int q = 0; q < XQ; ++q)
-                *reinterpret_cast<f32x4*>(&s_xi[wv][4 * lane + 256 * q]) = xr[q];
+                for (int q = 0; q < XQ; ++q)
+                    *reinterpret_cast<f32x4*>(&s_xi[wv][4 * lane + 256 * q]) = xr[q];
+            }
+        } else {
+            uint64_t key[KS];
+            const int seen = scan_row<KS, NP>(row, plane, n, ld, i, key);
+            GLL_TRACE_PT(16);
+            if constexpr (XL) {
+#pragma unroll
+                for (int q = 0; q < XQ; ++q)
+                    *reinterpret_cast<f32x4*>(&s_xi[wv][4 * lane + 256 * q]) = xr[q];
+            }
+            redo = merge_threshold<KS>(key, kc, seen, s_cand[wv], s_cgd[wv], ci, kce, tb, gb);
         }
-        const bool redo = merge_threshold<KS>(key, kc, seen, s_cand[wv], s_cgd[wv], ci, kce, tb, gb);
         GLL_TRACE_PT(17);
         if (redo) {
             if (lane == 0) atomicAdd(&status_pub[GLL_ST_KNN_MERGE], 1);
@@ -1300,6 +1472,14 @@ void knn_select_kernel(
             ci = merge_exact<KC>(full, kc, tb, gb);
             kce = kc;
         }
+    }
+    if (diag == 1) {   // phase timing (GLL_SEL_DIAG, diagnostic): candidates only; the row
+        if (lane < K) {  // keeps self loops only (valid indices, no edges downstream)
+            knn_idx[size_t(i) * K + lane] = ci >= -1 ? i : 0;
+            knn_d2[size_t(i) * K + lane] = 0.f;
+        }
+        if (lane == 0) eps[i] = 1.f;
+        return;
     }
     // 2b) drop the candidates the Gram's error bound already rules out, before their exact
     //     distances are computed (each is a d-float row gather): with G = the (K-1)-th smallest
@@ -1347,6 +1527,14 @@ void knn_select_kernel(
     double ce = double(exact_d2<VEC, PG, float, NU, XL>(X, xi, i, d, ci, 0, kce,
                                                         __builtin_inff(), &s_xi[wv][0]));
     GLL_TRACE_PT(18);
+    if (diag == 2) {   // phase timing: candidates, prune and exact distances (as diag 1)
+        if (lane < K) {
+            knn_idx[size_t(i) * K + lane] = ce >= -1.0 ? i : 0;
+            knn_d2[size_t(i) * K + lane] = 0.f;
+        }
+        if (lane == 0) eps[i] = 1.f;
+        return;
+    }
     if (ci < 0) ce = __builtin_inf();
     // 4) rank the candidates by (exact d^2, index); keep the K-1 nearest
     int rank = key_rank(ce, ci, kce);
@@ -1705,10 +1893,12 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     if (margin > 8) margin = 8;
     int kc = K - 1 + margin;
     if (kc > n - 1) kc = n - 1;
-    dim3 grid((n + 3) / 4, bt.B);
-    prof_begin(GLL_K_SELECT, s);
+    static const int hold = getenv("GLL_SEL_HOLD") ? atoi(getenv("GLL_SEL_HOLD")) : 1;  // A/B
+    static const int diag = getenv("GLL_SEL_DIAG") ? atoi(getenv("GLL_SEL_DIAG")) : 0;
     const size_t plane = size_t(n) * L.ldD;
     const int planes = gram_planes(L, bt.B);
+    dim3 grid((n + 3) / 4, bt.B);
+    prof_begin(GLL_K_SELECT, s);
 // Batched launches (PG = 1) stage x_i in LDS (XQ quarters of 256 features, d <= 1024) and run at
 // 6 waves per SIMD: measured at B = 64 NS, select 259 -> 214 us (XQ = 2, NU = 8; the NU = 16
 // batch of loads held 120 VGPRs, 4 waves).  NU: 32-feature steps per exact-distance load batch,
@@ -1717,14 +1907,21 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
 // Batched launches number blocks XCD-contiguously (R = true: each XCD works through a run of
 // graphs): NS B = 64 220 -> 213 us, FullySup B = 64 440 -> 429 us (profiles/r02h_xcd_ab.txt),
 // once the kernel took its graph index once instead of per pointer.
-#define GLL_SEL4(KCV, V, NPV, NUS, NUB, XQV)                                                   \
-    launch_k((bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2, NUS>                               \
-                        : knn_select_kernel<KCV, V, NPV, 1, NUB, (V ? XQV : 0), true>), grid, 256, 0, s, \
+#define GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, CHV)                                              \
+    launch_k((bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2, NUS, 0, false, CHV>                \
+                        : knn_select_kernel<KCV, V, NPV, 1, NUB, (V ? XQV : 0), true, CHV>), grid, 256, 0, s, \
         L.at<float>(ws, L.D2), L.ldD, plane, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0,     \
         L.RCAP,                                                                                \
         L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \
         L.at<int32_t>(ws, L.rev_cnt), L.at<int32_t>(ws, L.rev_idx), L.at<float>(ws, L.rev_d2), \
-        L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub, bt.x, bt.ws, bt.st)
+        L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub, bt.x, bt.ws, bt.st, diag)
+// the threshold scan holds rows of <= 2048 columns in registers (KC <= 32, aligned d)
+#define GLL_SEL4(KCV, V, NPV, NUS, NUB, XQV)                                                   \
+    do {                                                                                       \
+        if (KCV <= 32 && V && hold && n <= 1024) GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, (KCV <= 32 && V ? 1 : 0)); \
+        else if (KCV <= 32 && V && hold && n <= 2048) GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, (KCV <= 32 && V ? 2 : 0)); \
+        else GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, 0);                                          \
+    } while (0)
 #define GLL_SEL(KCV, V)                                                                        \
     do {                                                                                       \
         if (planes == 2) GLL_SEL4(KCV, V, 2, 16, 16, 0);                                       \
@@ -1739,6 +1936,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     else { if (vec) GLL_SEL(64, true); else GLL_SEL(64, false); }
 #undef GLL_SEL
 #undef GLL_SEL4
+#undef GLL_SEL5
     prof_end(GLL_K_SELECT, s);
     return launch_status("knn.hip:launch_select");
 }
