@@ -293,15 +293,16 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
 # ----------------------------------------------------------------------------------------
 # knn_sym_dist: device graph, returned as the reference's scipy objects
 # ----------------------------------------------------------------------------------------
-def device_graph(X: torch.Tensor, k: int = DEFAULT_K, epsilon="auto"):
+def device_graph(X: torch.Tensor, k: int = DEFAULT_K, epsilon="auto", flags: int = 0):
     """Build the symmetric kNN graph on the GPU; returns a dict of device tensors
-    (knn_idx, knn_d2, eps, row_ptr, col, w, d2, deg)."""
+    (knn_idx, knn_d2, eps, row_ptr, col, w, d2, deg).  `flags`: gll_problem.flags
+    (e.g. _lib.FLAG_KNN_PANEL, row panels instead of the n x n distances)."""
     _check_k(k, X.shape[0])
     dev = _device_for(X)
     n, d = X.shape
     with torch.cuda.device(dev):
         X32 = _features(X, dev)
-        prob = make_problem(n, d, 0, 1, k, 0.0, epsilon)
+        prob = make_problem(n, d, 0, 1, k, 0.0, epsilon, flags=flags)
         nbytes = _lib.lib().gll_workspace_bytes(ct.byref(prob))
         if nbytes == 0:
             raise ValueError(f"unsupported graph problem n={n} d={d} k={k}")

@@ -127,10 +127,24 @@ static int build_graph(const gll_problem* p, const Layout& L, const Batch& bt, c
                        const void* Y, int y_dtype, void* ws, hipStream_t s) {
     const bool vec = vec_ok(X, p->d);
     const bool auto_eps = !(p->eps > 0.f);
-    if (launch_gram(L, bt, ws, X, vec, s) != hipSuccess) return GLL_ERR_HIP;
-    if (launch_select(L, bt, ws, X, p->eps, auto_eps, vec, public_status(p, L, ws), s) !=
-        hipSuccess)
-        return GLL_ERR_HIP;
+    if (L.PR < L.n) {
+        // row panels (Layout::PR < n: the n x n distances would not fit, or GLL_FLAG_KNN_PANEL):
+        // each panel's rows against every column, then their selection; the reverse lists and
+        // status counters accumulate across panels (reset by the first panel's Gram)
+        if (bt.B > 1) return GLL_ERR_UNSUPPORTED;
+        for (int r0 = 0; r0 < L.n; r0 += L.PR) {
+            const int rows = L.n - r0 < L.PR ? L.n - r0 : L.PR;
+            if (launch_gram_panel(L, ws, X, vec, r0, rows, s) != hipSuccess) return GLL_ERR_HIP;
+            if (launch_select(L, bt, ws, X, p->eps, auto_eps, vec, public_status(p, L, ws), s,
+                              r0, rows) != hipSuccess)
+                return GLL_ERR_HIP;
+        }
+    } else {
+        if (launch_gram(L, bt, ws, X, vec, s) != hipSuccess) return GLL_ERR_HIP;
+        if (launch_select(L, bt, ws, X, p->eps, auto_eps, vec, public_status(p, L, ws), s) !=
+            hipSuccess)
+            return GLL_ERR_HIP;
+    }
     return hip_status(launch_finalize(L, bt, ws, Y, y_dtype, p->tau, auto_eps ? 0.f : p->eps, s));
 }
 

@@ -137,6 +137,24 @@ inline int gram_splits(int n, int d) {
     return ((n + 63) / 64 <= 16 && d > 256 && d <= 512) ? 2 : 1;
 }
 
+// Rows of the squared-distance buffer: n (the whole n x n matrix), or a panel of PR rows when
+// the matrix would pass 32 GiB (panels of 8 GiB) or GLL_FLAG_KNN_PANEL asks for panels of 1,024
+// rows (GLL_PANEL_ROWS overrides both; diagnostic).  The kNN is then built panel by panel:
+// rectangular Gram tiles of the panel's rows against every column, then the select of those
+// rows (api.hip build_graph).  A multiple of 128 (the Gram tile), < n in panel mode.
+inline int panel_rows(int n, int flags) {
+    const size_t row_bytes = size_t((n + 3) & ~3) * 4;
+    static const int env = getenv("GLL_PANEL_ROWS") ? atoi(getenv("GLL_PANEL_ROWS")) : 0;
+    int64_t pr = n;
+    if (env > 0) pr = env;
+    else if (flags & GLL_FLAG_KNN_PANEL) pr = 1024;
+    else if (size_t(n) * row_bytes > (size_t(32) << 30)) pr = int64_t((size_t(8) << 30) / row_bytes);
+    if (pr >= n) return n;
+    pr = (pr / 128) * 128;
+    if (pr < 128) pr = 128;
+    return pr < n ? int(pr) : n;
+}
+
 size_t grid_cg_workspace_floats(int m, int C);
 struct Layout;
 int ell_emit(const Layout& L, int B);
@@ -146,6 +164,7 @@ struct Layout {
     int flags;        // gll_problem.flags
     int KS;           // Gram split planes (gram_splits)
     int ldD;          // leading dimension of the n x n squared-distance matrix
+    int PR;           // rows of the distance buffer (panel_rows: n, or a panel < n)
     int RCAP;         // reverse-list capacity per row
     int Wcap;         // slot width of a row
     int64_t Etot;     // entry capacity: n Wcap slots + 2 n (K-1) bump region
@@ -166,7 +185,8 @@ struct Layout {
         K = p.K < p.n ? p.K : p.n;
         m = n - base;
         ldD = (n + 3) & ~3;
-        KS = gram_splits(n, d);
+        PR = panel_rows(n, flags);
+        KS = PR < n ? 1 : gram_splits(n, d);
         RCAP = 4 * (K - 1) + 8;
         Wcap = (K - 1) + RCAP;
         Etot = int64_t(n) * Wcap + 2LL * n * (K - 1);
@@ -177,7 +197,7 @@ struct Layout {
             return at;
         };
         status = take(GLL_ST_NWORDS * 4);
-        D2 = take(size_t(KS) * n * ldD * 4);   // KS partial planes
+        D2 = take(size_t(KS) * PR * ldD * 4);  // KS partial planes (or one panel)
         knn_idx = take(size_t(n) * K * 4);
         knn_d2 = take(size_t(n) * K * 4);
         eps = take(size_t(n) * 4);
@@ -239,6 +259,7 @@ inline int gram_planes(const Layout& L, int B) {
 // Device helpers
 // ---------------------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
@@ -517,9 +538,12 @@ void prof_end(int kid, hipStream_t s);
 
 hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
                        hipStream_t s);
+// rows r0 .. r0 + rows - 1 of the graph (a panel, D2 holding only them); rows < 0: every row
 hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float* X,
                          float eps_fixed, bool auto_eps, bool vec, int32_t* status_pub,
-                         hipStream_t s);
+                         hipStream_t s, int r0 = 0, int rows = -1);
+hipError_t launch_gram_panel(const Layout& L, void* ws, const float* X, bool vec, int r0, int rows,
+                             hipStream_t s);
 hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,
                            int y_dtype, float tau, float eps_fixed, hipStream_t s);
 // b: right-hand sides of graph 0, `b_stride` bytes apart (the workspace rhs or gbar)

@@ -418,7 +418,10 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
                                                          int d, int T, float* __restrict__ D2,
                                                          int ld, int32_t* __restrict__ status,
                                                          int32_t* __restrict__ rev_cnt,
-                                                         size_t xs, size_t wss) {
+                                                         size_t xs, size_t wss, int r0,
+                                                         int pt) {
+    // pt > 0 (a row panel, build_graph): rectangular tiles of rows r0 .. r0 + 128 pt against
+    // every column block, stored in the direct orientation only into the panel's rows of D2
     X = gshift_br(X, xs);
     D2 = gshift_br(D2, wss);
     status = gshift_br(status, wss);
@@ -432,13 +435,18 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
-    int bi = 0, rem = xcd_tile(bx(), gridDim.x);
-    while (rem >= T - bi) {
-        rem -= T - bi;
-        ++bi;
+    int bi = 0, rem = xcd_tile(bx(), gridDim.x), bj;
+    if (pt > 0) {
+        bi = (r0 >> 7) + rem / T;
+        bj = rem % T;
+    } else {
+        while (rem >= T - bi) {
+            rem -= T - bi;
+            ++bi;
+        }
+        bj = bi + rem;
     }
-    const int bj = bi + rem;
-    {   // per-call reset of the counters the select kernel accumulates into
+    if (r0 == 0) {   // per-call reset of the counters the select kernel accumulates into
         const int g = bx() * 1024 + tid;
         if (g < GLL_ST_NWORDS) status[g] = 0;
         for (int q = g; q < n; q += gridDim.x * 1024) rev_cnt[q] = 0;
@@ -525,7 +533,14 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
         const int rr = (e & 3) + 8 * (e >> 2) + 4 * h;
         dv[e] = nrm[32 * sa + rr] + nrm[128 + 32 * sb + r] - 2.f * acc[e];
     }
-    if (bi != bj) {
+    if (pt > 0) {   // panel: every tile in the direct orientation, rows relative to r0
+        const int j = j0 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int i = i0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            if (i < n && j < n) D2[size_t(i - r0) * ld + j] = dv[e];
+        }
+    } else if (bi != bj) {
         // direct orientation: element e is (i0 + rr, j0 + r) -- 32 lanes per 128-B row piece
         const int j = j0 + r;
 #pragma unroll
@@ -1399,7 +1414,7 @@ void knn_select_kernel(
     float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ rev_cnt,
     int32_t* __restrict__ rev_idx, float* __restrict__ rev_d2, int32_t* __restrict__ ovf,
     int32_t* __restrict__ status, int32_t* __restrict__ status_pub, size_t xs, size_t wss,
-    size_t sts, int diag) {
+    size_t sts, int diag, int r0, int r1) {
     GLL_TRACE_SCOPE(1);
     GLL_TRACE_PT(20);
     const int2 gxy = batch_xy<R>();   // once (per pointer it re-reads gridDim and divides)
@@ -1420,8 +1435,8 @@ void knn_select_kernel(
     __shared__ float s_xi[XL ? 4 : 1][XL ? 256 * XQ : 1];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
-    const int i = gxy.x * 4 + wv;
-    if (i >= n) return;  // whole wave
+    const int i = r0 + gxy.x * 4 + wv;   // rows r0 .. r1 - 1: all, or a panel (D2 row i - r0)
+    if (i >= r1) return;  // whole wave
     // XL: x_i is staged once in LDS (its loads ride under the D2 scan's), so the exact
     // distances hold only the candidates' rows in registers (occupancy) and do not re-load x_i
     // per sweep.  Features past d are zero (masked at use anyway).
@@ -1437,7 +1452,7 @@ void knn_select_kernel(
 
     // 1-2) candidates: short per-lane lists + threshold merge, exact re-run when inexact.
     //      tb: D2 bits every non-candidate column is >= to (+inf: all valid columns taken)
-    const float* row = D2 + size_t(i) * ld;
+    const float* row = D2 + size_t(i - r0) * ld;
     constexpr int KS = KC <= 16 ? 4 : 8;
     int ci, kce;
     uint32_t tb, gb;   // gb: this lane's candidate's Gram D2 bits
@@ -1864,9 +1879,9 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         const dim3 grid(T * (T + 1) / 2, bt.B);
         prof_begin(GLL_K_GRAM, s);
         if (vec)
-            launch_k(gram_bf3w_kernel<true>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
+            launch_k(gram_bf3w_kernel<true>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws, 0, 0);
         else
-            launch_k(gram_bf3w_kernel<false>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws);
+            launch_k(gram_bf3w_kernel<false>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc, bt.x, bt.ws, 0, 0);
         prof_end(GLL_K_GRAM, s);
         return launch_status("knn.hip:launch_gram(bf3w)");
     }
@@ -1881,9 +1896,32 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
     return launch_status("knn.hip:launch_gram(bf3)");
 }
 
+// One row panel of the Gram (build_graph's panel mode, single graphs): rows r0 .. r0 + rows - 1
+// against every column on the inline-split 128-tile kernel (rectangular tiles: twice the flops
+// of the triangle, for an O(panel x n) buffer).
+hipError_t launch_gram_panel(const Layout& L, void* ws, const float* X, bool vec, int r0, int rows,
+                             hipStream_t s) {
+    float* D2 = L.at<float>(ws, L.D2);
+    int32_t* st = L.at<int32_t>(ws, L.status);
+    int32_t* rc = L.at<int32_t>(ws, L.rev_cnt);
+    const int T = (L.n + 127) / 128, pt = (rows + 127) / 128;
+    if (r0 % 128 || pt <= 0) return hipErrorInvalidValue;
+    const dim3 grid(unsigned(int64_t(pt) * T));
+    prof_begin(GLL_K_GRAM, s);
+    if (vec)
+        launch_k(gram_bf3w_kernel<true>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc,
+                 size_t(0), size_t(0), r0, pt);
+    else
+        launch_k(gram_bf3w_kernel<false>, grid, 1024, 0, s, X, L.n, L.d, T, D2, L.ldD, st, rc,
+                 size_t(0), size_t(0), r0, pt);
+    prof_end(GLL_K_GRAM, s);
+    return launch_status("knn.hip:launch_gram_panel");
+}
+
 hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float* X,
                          float eps_fixed, bool auto_eps, bool vec, int32_t* status_pub,
-                         hipStream_t s) {
+                         hipStream_t s, int r0, int rows) {
+    if (rows < 0) rows = L.n - r0;
     const int n = L.n, K = L.K;
     // candidate list capacity: smallest of {16, 32, 64} leaving a re-rank margin >= 4
     const int need = K - 1 + 4;
@@ -1897,7 +1935,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     static const int diag = getenv("GLL_SEL_DIAG") ? atoi(getenv("GLL_SEL_DIAG")) : 0;
     const size_t plane = size_t(n) * L.ldD;
     const int planes = gram_planes(L, bt.B);
-    dim3 grid((n + 3) / 4, bt.B);
+    dim3 grid((rows + 3) / 4, bt.B);
     prof_begin(GLL_K_SELECT, s);
 // Batched launches (PG = 1) stage x_i in LDS (XQ quarters of 256 features, d <= 1024) and run at
 // 6 waves per SIMD: measured at B = 64 NS, select 259 -> 214 us (XQ = 2, NU = 8; the NU = 16
@@ -1914,12 +1952,13 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
         L.RCAP,                                                                                \
         L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \
         L.at<int32_t>(ws, L.rev_cnt), L.at<int32_t>(ws, L.rev_idx), L.at<float>(ws, L.rev_d2), \
-        L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub, bt.x, bt.ws, bt.st, diag)
+        L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub, bt.x, bt.ws, bt.st, diag, \
+        r0, r0 + rows)
 // the threshold scan holds rows of <= 2048 columns in registers (KC <= 32, aligned d)
 #define GLL_SEL4(KCV, V, NPV, NUS, NUB, XQV)                                                   \
     do {                                                                                       \
-        if (KCV <= 32 && V && hold && n <= 1024) GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, (KCV <= 32 && V ? 1 : 0)); \
-        else if (KCV <= 32 && V && hold && n <= 2048) GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, (KCV <= 32 && V ? 2 : 0)); \
+        if (KCV <= 32 && V && hold && n <= 1024 && rows == n) GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, (KCV <= 32 && V ? 1 : 0)); \
+        else if (KCV <= 32 && V && hold && n <= 2048 && rows == n) GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, (KCV <= 32 && V ? 2 : 0)); \
         else GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, 0);                                          \
     } while (0)
 #define GLL_SEL(KCV, V)                                                                        \

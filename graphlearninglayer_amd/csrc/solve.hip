@@ -711,6 +711,384 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
 }
 
 // --------------------------------------------------------------------------------------
+// Column-pair CG for batches (cg_ell2_kernel, round 3): NC right-hand-side columns of one graph
+// per workgroup, the Chronopoulos-Gear recurrences of cg_ell_body MODE 1 run per column.
+// Batched launches are throughput-bound: B x C workgroups of the one-column kernel hold the
+// same ELL slices in registers C times over and issue one 4-B LDS gather per entry and column.
+// Here the published vectors are interleaved ([u][NC] floats), so one gather of NC x 4 B serves
+// every column, the ELL slice is loaded and held once per NC columns, and the NC columns' three
+// dot products share one LDS exchange and barrier.  Each column keeps its own step sizes,
+// convergence test and iteration count; a finished column is frozen (its x never changes
+// again) while the others go on.  Per column the arithmetic -- slot order, the DPP and LDS
+// reduction order, the recurrences -- is cg_ell_body MODE 1's, so the solutions are bitwise
+// those of the one-column kernel.
+// --------------------------------------------------------------------------------------
+template <int NT, int N>
+__device__ __forceinline__ void block_sumN(float (&v)[N], float* red, int& phase) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = dpp_add<0xB1, 0xf>(v[k]);
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = dpp_add<0x4E, 0xf>(v[k]);
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = dpp_add<0x141, 0xf>(v[k]);
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = dpp_add<0x140, 0xf>(v[k]);
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = dpp_add<0x142, 0xa>(v[k]);
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = dpp_add<0x143, 0xc>(v[k]);
+    constexpr int NW = NT / kWave;
+    constexpr int NQ = NW < 4 ? 4 : NW;
+    float* q = red + phase * N * NQ;
+    phase ^= 1;
+    if (lane_id() == 63) {
+        const int w = threadIdx.x >> 6;
+#pragma unroll
+        for (int k = 0; k < N; ++k) q[k * NQ + w] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        float a = 0.f;
+        if constexpr (NW % 4 == 0) {
+#pragma unroll
+            for (int w = 0; w < NW; w += 4) {
+                const f32x4 va = *reinterpret_cast<const f32x4*>(q + k * NQ + w);
+                a += va.x; a += va.y; a += va.z; a += va.w;
+            }
+        } else {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) a += q[k * NQ + w];
+        }
+        v[k] = a;
+    }
+}
+
+template <int NC>
+struct vecN { using type = float; };
+template <>
+struct vecN<2> { using type = f32x2; };
+template <>
+struct vecN<4> { using type = f32x4; };
+
+template <int NT, int R, int S, typename TB, int NC>
+__global__ __launch_bounds__(NT) void cg_ell2_kernel(
+    int m, int C, int base, const int32_t* __restrict__ row_start,
+    const int32_t* __restrict__ row_len, const int32_t* __restrict__ ucnt,
+    const int32_t* __restrict__ col, const float* __restrict__ wv, const float* __restrict__ diag,
+    const TB* __restrict__ bsrc, double* __restrict__ out64, float* __restrict__ out32,
+    float rtol, int max_iter, int mat_cap, int32_t* __restrict__ st_nonconv,
+    int32_t* __restrict__ st_iters, const int32_t* __restrict__ ell_col,
+    const float* __restrict__ ell_w, size_t wss, size_t bs, size_t us, size_t sts) {
+    static_assert(NT > kWave, "block reductions assume several waves");
+    using VT = typename vecN<NC>::type;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int2 gxy = batch_xy<true>();
+    ell_col = gshift_at(ell_col, wss, gxy.y);
+    ell_w = gshift_at(ell_w, wss, gxy.y);
+    row_start = gshift_br_at(row_start, wss, gxy.y);
+    row_len = gshift_br_at(row_len, wss, gxy.y);
+    ucnt = gshift_at(ucnt, wss, gxy.y);
+    col = gshift_br_at(col, wss, gxy.y);
+    wv = gshift_br_at(wv, wss, gxy.y);
+    diag = gshift_at(diag, wss, gxy.y);
+    bsrc = gshift_at(bsrc, bs, gxy.y);
+    out64 = gshift_br_at(out64, us, gxy.y);
+    out32 = gshift_br_at(out32, wss, gxy.y);
+    st_nonconv = gshift_br_at(st_nonconv, sts, gxy.y);
+    st_iters = gshift_br_at(st_iters, sts, gxy.y);
+    const int c0 = gxy.x * NC;
+    const int tid = threadIdx.x;
+    float* red = smem;                                     // 2 x 3NC x 4+ floats of reduction
+    int* scan = reinterpret_cast<int*>(smem + 2 * 3 * NC * 8);   // 16 ints of scan scratch
+    VT* P_ = reinterpret_cast<VT*>(smem + 2 * 3 * NC * 8 + 16);  // published u, [u][NC]
+    const int mp4 = (m + 3) & ~3;
+    int* lcol = reinterpret_cast<int*>(P_ + mp4);          // overflow entries, compacted
+    float* lw = reinterpret_cast<float*>(lcol + mat_cap);
+    int urow[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) urow[q] = tid + NT * q;
+    int ec[R][S];
+    float ew[R][S];
+    int ost[R], olen[R], ulen[R];
+    float dg[R], mi[R];
+    float x[R][NC], r[R][NC], p[R][NC], sv[R][NC], bv[R][NC];
+    int tov = 0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int u = urow[q];
+        const int uc = u < m ? u : 0;
+        ulen[q] = ucnt[uc];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            ec[q][s] = ell_col[size_t(s) * m + uc];
+            ew[q][s] = ell_w[size_t(s) * m + uc];
+        }
+        dg[q] = diag[uc];
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+            bv[q][k] = c0 + k < C ? to_f32(bsrc[size_t(uc) * C + c0 + k]) : 0.f;
+    }
+    int longer = 0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        if (urow[q] >= m) ulen[q] = 0;
+        longer |= ulen[q] > S ? 1 : 0;
+    }
+    const bool has_ovf = __syncthreads_or(longer) != 0;
+    float rz[NC], bb[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) rz[k] = bb[k] = 0.f;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int u = urow[q];
+        if (u >= m) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                ec[q][s] = 0;
+                ew[q][s] = 0.f;
+            }
+            dg[q] = 0.f;
+        }
+        ost[q] = 0;
+        olen[q] = 0;
+        if (has_ovf && u < m) {
+            const int len = ulen[q];
+            ost[q] = row_start[base + u] + row_len[base + u] - len + S;
+            olen[q] = len - S;
+            tov += olen[q] > 0 ? olen[q] : 0;
+        }
+        mi[q] = 0.f;
+        VT pv;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            x[q][k] = r[q][k] = p[q][k] = sv[q][k] = 0.f;
+        }
+        if (u < m) {
+            mi[q] = dg[q] > 0.f ? 1.f / dg[q] : 0.f;
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                r[q][k] = mi[q] > 0.f ? bv[q][k] : 0.f;
+                p[q][k] = mi[q] * r[q][k];
+                rz[k] += r[q][k] * p[q][k];
+                bb[k] += r[q][k] * r[q][k];
+            }
+        }
+        if constexpr (NC == 1) pv = p[q][0];
+        else {
+#pragma unroll
+            for (int k = 0; k < NC; ++k) pv[k] = p[q][k];
+        }
+        if (u < m) P_[u] = pv;
+    }
+    int ov_total = 0;
+    int ooff = has_ovf ? block_excl_scan<NT>(tov, scan, ov_total) : 0;
+    const bool matl = ov_total <= mat_cap;
+    if (has_ovf && matl) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            for (int t = 0; t < olen[q]; ++t) {
+                const int e = ost[q] + t;
+                lcol[ooff + t] = col[e] - base;
+                lw[ooff + t] = wv[e];
+            }
+            if (olen[q] > 0) {
+                ost[q] = ooff;
+                ooff += olen[q];
+            }
+        }
+    }
+    int phase = 0;
+    __syncthreads();
+    int smax[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) smax[q] = wave_max_int(ulen[q] < S ? ulen[q] : S);
+    // (A y)_row for every column: diag y_row - sum W y_j, the one-column kernel's slot order
+    auto spmv = [&](int q, const float (&yq)[NC], float (&out)[NC]) {
+        VT pv[S];
+#pragma unroll
+        for (int s0 = 0; s0 < S; s0 += 4) {
+            if (s0 < smax[q]) {
+#pragma unroll
+                for (int t = 0; t < 4 && s0 + t < S; ++t) pv[s0 + t] = P_[ec[q][s0 + t]];
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4 && s0 + t < S; ++t) pv[s0 + t] = VT{};
+            }
+        }
+        float acc[NC];
+#pragma unroll
+        for (int k = 0; k < NC; ++k) acc[k] = 0.f;
+        auto add = [&](float wgt, VT v) {
+            if constexpr (NC == 1) acc[0] += wgt * v;
+            else {
+#pragma unroll
+                for (int k = 0; k < NC; ++k) acc[k] += wgt * v[k];
+            }
+        };
+#pragma unroll
+        for (int s2 = 0; s2 < S; ++s2) add(ew[q][s2], pv[s2]);
+        const int e0 = ost[q], no = olen[q];
+        if (matl) {
+            int t = 0;
+            for (; t + 4 <= no; t += 4) {
+                int c4[4];
+                float w4[4];
+                VT p4[4];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    c4[v] = lcol[e0 + t + v];
+                    w4[v] = lw[e0 + t + v];
+                }
+#pragma unroll
+                for (int v = 0; v < 4; ++v) p4[v] = P_[c4[v]];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) add(w4[v], p4[v]);
+            }
+            for (; t < no; ++t) add(lw[e0 + t], P_[lcol[e0 + t]]);
+        } else {
+            int t = 0;
+            for (; t + 4 <= no; t += 4) {
+                int c4[4];
+                float w4[4];
+                VT p4[4];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    c4[v] = col[e0 + t + v];
+                    w4[v] = wv[e0 + t + v];
+                }
+#pragma unroll
+                for (int v = 0; v < 4; ++v) p4[v] = P_[c4[v] - base];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) add(w4[v], p4[v]);
+            }
+            for (; t < no; ++t) add(wv[e0 + t], P_[col[e0 + t] - base]);
+        }
+#pragma unroll
+        for (int k = 0; k < NC; ++k) out[k] = dg[q] * yq[k] - acc[k];
+    };
+    // pre-step: s0 = A u0 (u0 = p, published), gamma0 = (r,u), delta0 = (s,u)
+    float tot[3 * NC];
+    {
+        float dl[NC];
+#pragma unroll
+        for (int k = 0; k < NC; ++k) dl[k] = 0.f;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            spmv(q, p[q], sv[q]);
+#pragma unroll
+            for (int k = 0; k < NC; ++k) dl[k] += p[q][k] * sv[q][k];
+        }
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            tot[3 * k] = rz[k];
+            tot[3 * k + 1] = bb[k];
+            tot[3 * k + 2] = dl[k];
+        }
+    }
+    block_sumN<NT, 3 * NC>(tot, red, phase);
+    float tol2[NC], gam[NC], alpha[NC];
+    bool act[NC], conv[NC];
+    int it[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        const float bbk = tot[3 * k + 1], dlk = tot[3 * k + 2];
+        tol2[k] = rtol * rtol * bbk;
+        conv[k] = !(bbk > 0.f);
+        gam[k] = tot[3 * k];
+        alpha[k] = dlk > 0.f ? gam[k] / dlk : 0.f;
+        if (!(dlk > 0.f)) alpha[k] = -1.f;
+        it[k] = 0;
+        act[k] = !conv[k] && alpha[k] > 0.f && it[k] < max_iter;
+    }
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) any |= act[k];
+    while (any) {
+        float ap[R][NC];
+#pragma unroll
+        for (int k = 0; k < NC; ++k) it[k] += act[k] ? 1 : 0;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            VT pv;
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                if (act[k]) {
+                    x[q][k] += alpha[k] * p[q][k];
+                    r[q][k] -= alpha[k] * sv[q][k];
+                }
+                ap[q][k] = act[k] ? mi[q] * r[q][k] : 0.f;
+                if constexpr (NC == 1) pv = ap[q][0];
+                else pv[k] = ap[q][k];
+            }
+            const int u = urow[q];
+            if (u < m) P_[u] = pv;
+        }
+        __syncthreads();
+        float w[R][NC];
+#pragma unroll
+        for (int k = 0; k < 3 * NC; ++k) tot[k] = 0.f;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            spmv(q, ap[q], w[q]);
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                tot[3 * k] += r[q][k] * ap[q][k];
+                tot[3 * k + 1] += w[q][k] * ap[q][k];
+                tot[3 * k + 2] += r[q][k] * r[q][k];
+            }
+        }
+        block_sumN<NT, 3 * NC>(tot, red, phase);
+        any = false;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            if (!act[k]) continue;
+            const float gn = tot[3 * k], de = tot[3 * k + 1], rr = tot[3 * k + 2];
+            if (rr <= tol2[k]) {
+                conv[k] = true;
+                act[k] = false;
+                continue;
+            }
+            const float beta = gn * __builtin_amdgcn_rcpf(gam[k]);
+            const float den = alpha[k] * de - beta * gn;
+            if (!(den > 0.f)) {   // breakdown or NaN: reported as non-converged
+                act[k] = false;
+                continue;
+            }
+            alpha[k] = (gn * alpha[k]) * __builtin_amdgcn_rcpf(den);
+            gam[k] = gn;
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                p[q][k] = ap[q][k] + beta * p[q][k];
+                sv[q][k] = w[q][k] + beta * sv[q][k];
+            }
+            act[k] = it[k] < max_iter && alpha[k] > 0.f;
+            any |= act[k];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int u = urow[q];
+        if (u < m) {
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                if (c0 + k >= C) continue;
+                if (out64) out64[size_t(u) * C + c0 + k] = double(x[q][k]);
+                if (out32) out32[size_t(u) * C + c0 + k] = x[q][k];
+            }
+        }
+    }
+    if (tid == 0) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            if (c0 + k >= C) continue;
+            if (st_iters) atomicMax(st_iters, it[k]);
+            if (!conv[k] && st_nonconv) atomicAdd(st_nonconv, 1);
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------------
 // Balanced per-column CG for long U rows (cg_vr_kernel).
 //
 // At K = 25 (the FullySup caller, FullySup.py:156) a U row of Luu holds 27 entries on average
@@ -1142,6 +1520,33 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
     return launch_status("solve.hip:run_ell");
 }
 
+template <int NT, int R, int S, typename TB, int NC>
+static hipError_t run_ell2(const Layout& L, const Batch& bt, void* ws, const TB* b, size_t bs,
+                           double* out64, float* out32, float rtol, int max_iter,
+                           int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
+    static_assert(NT <= 512, "reduction scratch sized for <= 8 waves");
+    size_t lds = size_t(2 * 3 * NC * 8 + 16) * 4 + size_t((L.m + 3) & ~3) * 4 * NC;
+    // overflow entries as run_ell caps them for batches (2048: several workgroups per CU)
+    const int64_t eu_bound = int64_t(L.m + L.n) * (L.K - 1);
+    int64_t cap = int64_t(kLdsDyn - lds) / 8;
+    if (cap > eu_bound) cap = eu_bound;
+    if (cap > 2048) cap = 2048;
+    if (cap < 0) cap = 0;
+    lds += size_t(cap) * 8;
+    if (S != ell_emit(L, bt.B)) {
+        (void)hipGetLastError();
+        return hipErrorInvalidValue;
+    }
+    auto fn = cg_ell2_kernel<NT, R, S, TB, NC>;
+    allow_full_lds(reinterpret_cast<const void*>(fn));
+    launch_k(fn, dim3((L.C + NC - 1) / NC, bt.B), NT, lds, s,
+        L.m, L.C, L.base, L.at<int32_t>(ws, L.row_start), L.at<int32_t>(ws, L.row_len),
+        L.at<int32_t>(ws, L.ucnt), L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
+        L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, int(cap), st_nonconv, st_iters,
+        L.at<int32_t>(ws, L.ell_col), L.at<float>(ws, L.ell_w), bt.ws, bs, bt.u, bt.st);
+    return launch_status("solve.hip:run_ell2");
+}
+
 // ---------------------------------------------------------------------------------------
 // Fused backward of one small graph (gll_backward, B = 1, fixed eps, C = 10, m <= 512: the
 // north-star shape).  The adjoint solve occupies C workgroups of the GPU for ~15 us while the
@@ -1506,6 +1911,22 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     if (m <= 512 && cg_nt == 128) GLL_ELL(128, 4, 24);
     if (m <= 512 && cg_nt == 256) GLL_ELL(256, 2, 24);
     if (m <= 512 && bt.B == 1) GLL_ELL(512, 1, 24);
+    // batches: column pairs (cg_ell2_kernel) where the default is the MODE 1 recurrence;
+    // GLL_FLAG_CG_NC1 or GLL_CG_NC = 1 keeps the one-column kernel (A/B), GLL_CG_NC = 4 four
+    // columns, GLL_CG_NT = 512 one row per thread
+    static const int cg_nc = getenv("GLL_CG_NC") ? atoi(getenv("GLL_CG_NC")) : 2;
+    if (m <= 512 && bt.B > 1 && cg_nc > 1 && cg_mode_env <= 1 &&
+        !(L.flags & (GLL_FLAG_CG_CLASSIC | GLL_FLAG_CG_PIPE | GLL_FLAG_CG_NC1))) {
+        if (cg_nt == 512)
+            return cg_nc == 4 ? run_ell2<512, 1, 24, TB, 4>(L, bt, ws, b, bs, out64, out32, rtol,
+                                                            max_iter, st_nonconv, st_iters, s)
+                              : run_ell2<512, 1, 24, TB, 2>(L, bt, ws, b, bs, out64, out32, rtol,
+                                                            max_iter, st_nonconv, st_iters, s);
+        return cg_nc == 4 ? run_ell2<256, 2, 24, TB, 4>(L, bt, ws, b, bs, out64, out32, rtol,
+                                                        max_iter, st_nonconv, st_iters, s)
+                          : run_ell2<256, 2, 24, TB, 2>(L, bt, ws, b, bs, out64, out32, rtol,
+                                                        max_iter, st_nonconv, st_iters, s);
+    }
     if (m <= 512) GLL_ELL(256, 2, 24);
     if (m <= 1024) GLL_ELL(1024, 1, 16);
     if (m <= 2048) GLL_ELL(1024, 2, 16);

@@ -75,6 +75,11 @@ extern "C" {
 #define GLL_FLAG_BWD_UNFUSED 16384 /* single small graphs, fixed eps: adjoint CG and feature
                                     * gradient as two launches instead of the fused one
                                     * (diagnostic) */
+#define GLL_FLAG_CG_NC1 32768      /* batched per-column CG: one right-hand-side column per
+                                    * workgroup instead of column pairs (diagnostic) */
+#define GLL_FLAG_KNN_PANEL 65536   /* single graphs: build the kNN in row panels of 1,024 rows
+                                    * (an O(panel x n) distance buffer instead of n x n; automatic
+                                    * past 32 GiB of n x n distances, panels of 8 GiB) */
 
 typedef struct gll_problem {
     int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */

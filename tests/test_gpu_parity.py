@@ -751,6 +751,112 @@ def _fwd_bwd_c_abi(X, Y, k, tau, eps, gbar, flags=0):
     return U.cpu().numpy(), gx.cpu().numpy()
 
 
+def _fwd_bwd_batched_c_abi(Xs, Ys, k, tau, eps, G, flags=0):
+    """gll_forward_batched + gll_backward_batched through ctypes: (U[B], grad_X[B], iterations)."""
+    import ctypes as ct
+    from graphlearninglayer_amd import _lib
+    GLL = _gll()
+    B, n, d = Xs.shape
+    base, C = Ys.shape[1:]
+    prob = GLL.make_problem(n, d, base, C, k, tau, eps, flags=flags)
+    lib = _lib.lib()
+    wb = lib.gll_workspace_bytes(ct.byref(prob))
+    ws = torch.empty(B * wb, dtype=torch.uint8, device="cuda")
+    U = torch.empty(B, n - base, C, dtype=torch.float64, device="cuda")
+    gx = torch.empty(B, n, d, dtype=torch.float32, device="cuda")
+    Xd = torch.from_numpy(np.ascontiguousarray(Xs)).cuda()
+    Yd = torch.from_numpy(np.ascontiguousarray(Ys)).cuda()
+    gd = torch.from_numpy(np.ascontiguousarray(G, dtype=np.float64)).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.check(lib.gll_forward_batched(ct.byref(prob), B, Xd.data_ptr(), Yd.data_ptr(),
+                                       _lib.GLL_DT_F32, ws.data_ptr(), U.data_ptr(), s),
+               "gll_forward_batched")
+    _lib.check(lib.gll_backward_batched(ct.byref(prob), B, Xd.data_ptr(), ws.data_ptr(),
+                                        gd.data_ptr(), _lib.GLL_DT_F64, gx.data_ptr(), s),
+               "gll_backward_batched")
+    torch.cuda.synchronize()
+    return U.cpu().numpy(), gx.cpu().numpy()
+
+
+@pytest.mark.parametrize("d,eps", [(64, 1.0), (256, "auto"), (100, "auto")])
+def test_knn_row_panels_match_whole_matrix(d, eps):
+    """kNN in row panels (GLL_FLAG_KNN_PANEL: 1,024-row panels of rectangular Gram tiles, each
+    panel selected before the next is computed -- the path graphs past 32 GiB of n x n distances
+    take) against the whole n x n matrix: the Gram only nominates candidates and the select is
+    exact, so the kNN lists, distances, eps, the CSR and then U and grad_X agree bitwise (ragged
+    last panel; d not a multiple of 64, and of 4: the scalar loads)."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
+    base, m, k = 900, 3300, 10
+    X, lab = synth(base, m, d, r=1.0, seed=31)
+    GLL = _gll()
+    Xd = torch.from_numpy(X).cuda()
+    gw = GLL.device_graph(Xd, k, eps)
+    gp = GLL.device_graph(Xd, k, eps, flags=_lib.FLAG_KNN_PANEL)
+    for key in ("knn_idx", "knn_d2", "eps", "row_ptr", "col", "w", "deg"):
+        assert torch.equal(gw[key], gp[key]), key
+    Y = one_hot(lab[:base])
+    g = seeded_gbar(m, 10, 77)
+    Uw, gxw = _fwd_bwd_c_abi(X, Y, k, 0.07, eps, g)
+    Up, gxp = _fwd_bwd_c_abi(X, Y, k, 0.07, eps, g, flags=_lib.FLAG_KNN_PANEL)
+    np.testing.assert_array_equal(Up, Uw)
+    np.testing.assert_array_equal(gxp, gxw)
+
+
+def test_knn_row_panels_automatic_past_the_n2_buffer():
+    """A graph whose n x n distances (40 GB at n = 100,000) pass the 32 GiB line: the workspace
+    holds an 8 GiB row panel instead (gll_workspace_bytes far below n^2 x 4), and the kNN of
+    sampled rows is the exact float64 kNN, as is eps for auto epsilon."""
+    import ctypes as ct
+    from graphlearninglayer_amd import _lib
+    n, d, k = 100_000, 64, 10
+    rng = np.random.default_rng(5)
+    centres = rng.standard_normal((50, d))
+    X = (centres[rng.integers(0, 50, n)] + 0.6 * rng.standard_normal((n, d))).astype(np.float32)
+    GLL = _gll()
+    prob = GLL.make_problem(n, d, 0, 1, k, 0.0, "auto")
+    nbytes = _lib.lib().gll_workspace_bytes(ct.byref(prob))
+    assert nbytes < n * n * 4 // 4, nbytes
+    g = GLL.device_graph(torch.from_numpy(X).cuda(), k, "auto")
+    ind = g["knn_idx"].cpu().numpy()
+    eps = g["eps"].cpu().numpy()
+    X64 = X.astype(np.float64)
+    for i in rng.choice(n, 48, replace=False):
+        d2 = np.sum((X64 - X64[i]) ** 2, axis=1)
+        d2[i] = np.inf
+        order = np.argsort(d2, kind="stable")[: k - 1]
+        got = ind[i, 1:]
+        assert ind[i, 0] == i
+        if set(order.tolist()) != set(got.tolist()):
+            # excused only at exact ties of the boundary distance
+            assert abs(np.max(d2[got]) - d2[order[-1]]) <= 1e-12 * d2[order[-1]], i
+        assert abs(eps[i] - np.sqrt(d2[order[-1]])) <= 1e-6 * np.sqrt(d2[order[-1]]), i
+
+
+@pytest.mark.parametrize("C", [10, 7])
+def test_batched_column_pair_cg_matches_one_column_kernel_bitwise(C):
+    """Batched per-column CG on column pairs (solve.hip cg_ell2_kernel, the default for batches
+    of m <= 512 graphs) against the one-column kernel (GLL_FLAG_CG_NC1): each column keeps its
+    own step sizes and convergence test and the same arithmetic order, so U and grad_X agree
+    bitwise -- also with an odd column count (a padding column in the last pair) -- and within
+    the parity bar of the float64 oracle (GLL.py:53,93)."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import seeded_gbar
+    B = 4
+    Xs, Ys, c = _synth_batch("ns", B, seed0=41)
+    Ys = np.ascontiguousarray(Ys[:, :, :C])
+    Ys[:, :, C - 1] += (Ys.sum(axis=2) == 0)   # every labeled row keeps one class
+    G = np.stack([seeded_gbar(c["batch"], C, 500 + g) for g in range(B)])
+    U2, g2 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G)
+    U1, g1 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G, flags=_lib.FLAG_CG_NC1)
+    np.testing.assert_array_equal(U2, U1)
+    np.testing.assert_array_equal(g2, g1)
+    ind = _gpu_knn(Xs[1], c["k"], 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, st = O.forward(Xs[1], Ys[1], tau=0.07, epsilon=1.0, K=c["k"], knn=(ind, None))
+    assert O.rel_err(U2[1], Uo) <= TOL
+    assert O.rel_err(g2[1], O.backward(st, G[1])) <= TOL
+
+
 @pytest.mark.parametrize("cfg,eps", [("ns", 1.0), ("ns", "auto"), ("fullysup", 1.0),
                                      ("stress", 1.0), ("stress", "auto")])
 def test_chunked_grad_matches_row_kernel_bitwise(cfg, eps):

@@ -63,6 +63,24 @@ def test_workspace_bytes_and_validation():
     assert lib.gll_strerror(-2).decode().startswith("unsupported")
 
 
+def test_workspace_row_panels():
+    """The distance buffer is n x n up to 32 GiB and a row panel past it (include/gll.h
+    GLL_FLAG_KNN_PANEL; gll_internal.h panel_rows): forced panels of 1,024 rows shrink the
+    workspace by the rows left out, small graphs never take panels, and at n = 100,000 (40 GB
+    of n x n distances) the workspace holds an 8 GiB panel instead."""
+    lib = _lib.lib()
+
+    def nbytes(n, d, flags=0):
+        return lib.gll_workspace_bytes(ct.byref(G.make_problem(n, d, 0, 1, 10, 0.0, 1.0,
+                                                               flags=flags)))
+    for n in (100, 1000, 1024):   # panels never shorter than the graph
+        assert nbytes(n, 64, _lib.FLAG_KNN_PANEL) == nbytes(n, 64)
+    whole, panel = nbytes(5000, 64), nbytes(5000, 64, _lib.FLAG_KNN_PANEL)
+    assert whole - panel == (5000 - 1024) * 5000 * 4
+    big = nbytes(100_000, 64)
+    assert 8 * 2**30 - 100_000 * 4 * 128 <= big < 9 * 2**30
+
+
 def test_entry_points_reject_bad_arguments_without_touching_the_gpu():
     lib = _lib.lib()
     p = G.make_problem(100, 16, 50, 10, 5, 0.0, 1.0)
