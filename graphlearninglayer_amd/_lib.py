@@ -29,7 +29,7 @@ FLAG_GRAD_ROWS = 2048   # gll_problem.flags: whole-row feature-gradient kernel (
 FLAG_GRAD_CHUNK = 4096  # gll_problem.flags: feature-chunked gradient kernel wherever it runs
 FLAG_GRAM_INLINE = 8192  # gll_problem.flags: 128-tile Gram with the inline split (diagnostic)
 FLAG_BWD_UNFUSED = 16384  # gll_problem.flags: adjoint CG and gradient as two launches (diagnostic)
-FLAG_CG_NC1 = 32768   # gll_problem.flags: batched per-column CG, one column per workgroup (diagnostic)
+FLAG_CG_PAIRS = 32768   # gll_problem.flags: batched per-column CG on column pairs (diagnostic)
 FLAG_KNN_PANEL = 65536   # gll_problem.flags: kNN in row panels (O(panel x n) distances)
 ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
 ST_KNN_RESCAN = 5   # kNN rows re-ranked over every column under the Gram error bound

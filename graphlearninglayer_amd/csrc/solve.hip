@@ -720,8 +720,10 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
 // dot products share one LDS exchange and barrier.  Each column keeps its own step sizes,
 // convergence test and iteration count; a finished column is frozen (its x never changes
 // again) while the others go on.  Per column the arithmetic -- slot order, the DPP and LDS
-// reduction order, the recurrences -- is cg_ell_body MODE 1's, so the solutions are bitwise
-// those of the one-column kernel.
+// reduction order, the recurrences -- is cg_ell_body MODE 1's, so the solutions are those of
+// the one-column kernel to fp32 contraction order.  Measured slower (B = 64 NS 21.6 -> 27.6 us
+// per launch, profiles/r03s_cg_pairs_ab.txt): the batched solve is bound by each workgroup's iteration
+// latency, not by the gathers and loads it saves, so it stays a diagnostic (GLL_FLAG_CG_PAIRS).
 // --------------------------------------------------------------------------------------
 template <int NT, int N>
 __device__ __forceinline__ void block_sumN(float (&v)[N], float* red, int& phase) {
@@ -1911,12 +1913,13 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     if (m <= 512 && cg_nt == 128) GLL_ELL(128, 4, 24);
     if (m <= 512 && cg_nt == 256) GLL_ELL(256, 2, 24);
     if (m <= 512 && bt.B == 1) GLL_ELL(512, 1, 24);
-    // batches: column pairs (cg_ell2_kernel) where the default is the MODE 1 recurrence;
-    // GLL_FLAG_CG_NC1 or GLL_CG_NC = 1 keeps the one-column kernel (A/B), GLL_CG_NC = 4 four
-    // columns, GLL_CG_NT = 512 one row per thread
-    static const int cg_nc = getenv("GLL_CG_NC") ? atoi(getenv("GLL_CG_NC")) : 2;
-    if (m <= 512 && bt.B > 1 && cg_nc > 1 && cg_mode_env <= 1 &&
-        !(L.flags & (GLL_FLAG_CG_CLASSIC | GLL_FLAG_CG_PIPE | GLL_FLAG_CG_NC1))) {
+    // batches: column pairs (cg_ell2_kernel) only on request (GLL_FLAG_CG_PAIRS; GLL_CG_NC = 2 / 4
+    // for A/B): measured slower -- B = 64 NS 21.6 -> 27.6 us per launch, B = 8 18.2 -> 25.1
+    // (profiles/r03s_cg_pairs_ab.txt): the batched solve is bound by each workgroup's iteration
+    // latency, which a second column lengthens, not by the LDS gathers it halves
+    static const int cg_nc = getenv("GLL_CG_NC") ? atoi(getenv("GLL_CG_NC")) : 1;
+    if (m <= 512 && bt.B > 1 && (cg_nc > 1 || (L.flags & GLL_FLAG_CG_PAIRS)) &&
+        cg_mode_env <= 1 && !(L.flags & (GLL_FLAG_CG_CLASSIC | GLL_FLAG_CG_PIPE))) {
         if (cg_nt == 512)
             return cg_nc == 4 ? run_ell2<512, 1, 24, TB, 4>(L, bt, ws, b, bs, out64, out32, rtol,
                                                             max_iter, st_nonconv, st_iters, s)
@@ -1927,6 +1930,13 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
                           : run_ell2<256, 2, 24, TB, 2>(L, bt, ws, b, bs, out64, out32, rtol,
                                                         max_iter, st_nonconv, st_iters, s);
     }
+    // batches of at most one column workgroup per CU (B x C <= 256) run the single-graph
+    // geometry, 512 x 1 with the Neumann form: NS B = 8 18.6 -> 15.9 us per launch; with more
+    // workgroups than CUs 256 x 2 (MODE 1) keeps the lead: B = 64 21.9 against 28.2 us
+    // (profiles/r03t_cg_batched_geometry_ab.txt).  GLL_CG_BNT = 512 / 256 forces one (A/B).
+    static const int cg_bnt = getenv("GLL_CG_BNT") ? atoi(getenv("GLL_CG_BNT")) : 0;
+    if (m <= 512 && (cg_bnt == 512 || (cg_bnt == 0 && int64_t(bt.B) * L.C <= 256)))
+        GLL_ELL(512, 1, 24);
     if (m <= 512) GLL_ELL(256, 2, 24);
     if (m <= 1024) GLL_ELL(1024, 1, 16);
     if (m <= 2048) GLL_ELL(1024, 2, 16);

@@ -75,8 +75,8 @@ extern "C" {
 #define GLL_FLAG_BWD_UNFUSED 16384 /* single small graphs, fixed eps: adjoint CG and feature
                                     * gradient as two launches instead of the fused one
                                     * (diagnostic) */
-#define GLL_FLAG_CG_NC1 32768      /* batched per-column CG: one right-hand-side column per
-                                    * workgroup instead of column pairs (diagnostic) */
+#define GLL_FLAG_CG_PAIRS 32768    /* batched per-column CG: two right-hand-side columns per
+                                    * workgroup (measured slower; diagnostic) */
 #define GLL_FLAG_KNN_PANEL 65536   /* single graphs: build the kNN in row panels of 1,024 rows
                                     * (an O(panel x n) distance buffer instead of n x n; automatic
                                     * past 32 GiB of n x n distances, panels of 8 GiB) */

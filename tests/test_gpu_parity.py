@@ -835,22 +835,24 @@ def test_knn_row_panels_automatic_past_the_n2_buffer():
 
 @pytest.mark.parametrize("C", [10, 7])
 def test_batched_column_pair_cg_matches_one_column_kernel_bitwise(C):
-    """Batched per-column CG on column pairs (solve.hip cg_ell2_kernel, the default for batches
-    of m <= 512 graphs) against the one-column kernel (GLL_FLAG_CG_NC1): each column keeps its
-    own step sizes and convergence test and the same arithmetic order, so U and grad_X agree
-    bitwise -- also with an odd column count (a padding column in the last pair) -- and within
-    the parity bar of the float64 oracle (GLL.py:53,93)."""
+    """Batched per-column CG on column pairs (solve.hip cg_ell2_kernel, GLL_FLAG_CG_PAIRS; a
+    measured-slower diagnostic variant) against the default one-column kernel: each column keeps
+    its own step sizes, convergence test and summation order, so U and grad_X agree to fp32
+    rounding (the compiler contracts a few multiply-adds of the two-column form differently:
+    at B = 40, 0.07% of U differ by <= 2.2e-7 relative) -- also with an odd column count (a
+    padding column in the last pair) -- and within the parity bar of the float64 oracle
+    (GLL.py:53,93)."""
     from graphlearninglayer_amd import _lib
     from graphlearninglayer_amd.synth import seeded_gbar
-    B = 4
+    B = 40   # B x C > 256: the default batched geometry is 256 x 2 with the MODE 1 recurrence
     Xs, Ys, c = _synth_batch("ns", B, seed0=41)
     Ys = np.ascontiguousarray(Ys[:, :, :C])
     Ys[:, :, C - 1] += (Ys.sum(axis=2) == 0)   # every labeled row keeps one class
     G = np.stack([seeded_gbar(c["batch"], C, 500 + g) for g in range(B)])
-    U2, g2 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G)
-    U1, g1 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G, flags=_lib.FLAG_CG_NC1)
-    np.testing.assert_array_equal(U2, U1)
-    np.testing.assert_array_equal(g2, g1)
+    U2, g2 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G, flags=_lib.FLAG_CG_PAIRS)
+    U1, g1 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G)
+    assert O.rel_err(U2, U1) <= 1e-6
+    assert O.rel_err(g2, g1) <= 1e-6
     ind = _gpu_knn(Xs[1], c["k"], 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
     Uo, st = O.forward(Xs[1], Ys[1], tau=0.07, epsilon=1.0, K=c["k"], knn=(ind, None))
     assert O.rel_err(U2[1], Uo) <= TOL
