@@ -31,6 +31,7 @@ FLAG_GRAM_INLINE = 8192  # gll_problem.flags: 128-tile Gram with the inline spli
 FLAG_BWD_UNFUSED = 16384  # gll_problem.flags: adjoint CG and gradient as two launches (diagnostic)
 FLAG_CG_PAIRS = 32768   # gll_problem.flags: batched per-column CG on column pairs (diagnostic)
 FLAG_KNN_PANEL = 65536   # gll_problem.flags: kNN in row panels (O(panel x n) distances)
+FLAG_D2_F32 = 131072   # gll_problem.flags: fp32 distance matrix on the pre-split Gram route (diagnostic)
 ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
 ST_KNN_RESCAN = 5   # kNN rows re-ranked over every column under the Gram error bound
 ST_SOLVE_FAILED = 6   # a whole-GPU CG lost a grid barrier: outputs NaN, raised as an error

@@ -27,6 +27,8 @@
 
 #include <type_traits>
 
+#include <atomic>
+
 #include "gll_internal.h"
 
 namespace gll {
@@ -69,6 +71,26 @@ __device__ __forceinline__ int xcd_tile(int b, int nt) {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+
+// D2 storage of the pre-split path (round 3): fp16 of D2 x s, s = 2^e per graph with every
+// D2 <= 4 max|a|^2 mapped below 2^14 (d2_scale), or fp32 (H = false).  D2 only nominates
+// candidates; the select decodes x 1/s (exact) and widens its error bounds by the fp16 rounding.
+template <bool H>
+__device__ __forceinline__ void dput(float* D2, size_t o, float v, float s) {
+    if constexpr (H) reinterpret_cast<_Float16*>(D2)[o] = static_cast<_Float16>(v * s);
+    else D2[o] = v;
+}
+template <bool H>
+__device__ __forceinline__ void dput4(float* D2, size_t o, f32x4 v, float s) {
+    if constexpr (H) {
+        const h16x4 hv = {static_cast<_Float16>(v.x * s), static_cast<_Float16>(v.y * s),
+                          static_cast<_Float16>(v.z * s), static_cast<_Float16>(v.w * s)};
+        *reinterpret_cast<h16x4*>(reinterpret_cast<_Float16*>(D2) + o) = hv;
+    } else {
+        *reinterpret_cast<f32x4*>(D2 + o) = v;
+    }
+}
 constexpr int kBP = 256;            // features per phase
 constexpr int kMaxCen = 4096;       // LDS copy of the centre row: d <= 4096 (gll.h limit)
 constexpr int kBS = kBP + 8;        // LDS plane row stride (bf16)
@@ -602,6 +624,18 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
 constexpr int kPK = 64;                  // features per k-stage
 typedef __attribute__((address_space(3))) void lds_void;
 
+// fp16 D2 scale of a graph from its gram_split word: s = 2^(14 - e) with 4 max|a|^2 < 2^e, so
+// every stored D2 x s stays below 2^14 (fp16 max 65504); 1 for an all-zero or non-finite graph.
+__device__ __forceinline__ float d2_scale(unsigned long long w) {
+    const float t = 4.f * __uint_as_float(uint32_t(w & 0xFFFFFFull) << 8);
+    if (!(t > 1e-30f) || !(t < 1e38f)) return 1.f;
+    int e;
+    (void)frexpf(t, &e);   // t = f 2^e, f in [0.5, 1)
+    int k = 14 - e;
+    k = k < -120 ? -120 : (k > 120 ? 120 : k);
+    return ldexpf(1.f, k);
+}
+
 template <bool VEC>
 __global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict__ X, int n, int d,
                                                          int dp, __bf16* __restrict__ Ph,
@@ -609,8 +643,11 @@ __global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict
                                                          float* __restrict__ nrm,
                                                          int32_t* __restrict__ status,
                                                          int32_t* __restrict__ rev_cnt,
-                                                         size_t xs, size_t wss) {
+                                                         size_t xs, size_t wss,
+                                                         unsigned long long* __restrict__ d2s,
+                                                         unsigned long long gen) {
     X = gshift_br(X, xs);
+    d2s = gshift_br(d2s, wss);
     Ph = gshift_br(Ph, wss);
     Pl = gshift_br(Pl, wss);
     nrm = gshift_br(nrm, wss);
@@ -623,7 +660,12 @@ __global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict
     }
     const int lane = lane_id();
     const int i = bx() * 4 + (threadIdx.x >> 6);
-    if (i >= n) return;
+    __shared__ unsigned s_key[4];
+    if (i >= n) {
+        if (lane == 0) s_key[threadIdx.x >> 6] = 0u;
+        __syncthreads();
+        return;
+    }
     const float* xi = X + size_t(i) * d;
     float sq = 0.f;
     for (int k = 4 * lane; k < dp; k += 4 * kWave) {
@@ -641,7 +683,19 @@ __global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict
         *reinterpret_cast<bf16x4*>(Pl + size_t(i) * dp + k) = lv;
     }
     sq = wave_sum_dpp(sq);
-    if (lane == 0) nrm[i] = sq;
+    if (lane == 0) {
+        nrm[i] = sq;
+        // |a_i|^2 rounded up to 24 bits of its float pattern (>= the value; NaN orders last)
+        const uint32_t b = __float_as_uint(sq > 0.f ? sq : 0.f) & 0x7FFFFFFFu;
+        s_key[threadIdx.x >> 6] = (b + 0xFFu) >> 8;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {   // the graph's max |a|^2 for the fp16 D2 scale, tagged with the
+        unsigned k = s_key[0];  // call's generation so an earlier call's word never wins
+#pragma unroll
+        for (int q = 1; q < 4; ++q) k = s_key[q] > k ? s_key[q] : k;
+        atomicMax(d2s, (gen << 24) | (unsigned long long)k);
+    }
 }
 
 // Tile t of the upper triangle of T x T blocks in supertile order: supertiles of kSR x kSC
@@ -681,11 +735,13 @@ __device__ __forceinline__ void supertile_tile(int t, int T, int& bi, int& bj) {
 
 // One-dimensional grid over B graphs x T (T + 1) / 2 tiles: xcd_tile deals each XCD a
 // contiguous run of the graph-major sequence, so a batch's graphs are XCD-local too.
+template <bool H>
 __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__ Ph,
                                                       const __bf16* __restrict__ Pl,
                                                       const float* __restrict__ nrm, int n,
                                                       int dp, int T, float* __restrict__ D2,
-                                                      int ld, size_t wss) {
+                                                      int ld, size_t wss,
+                                                      const unsigned long long* __restrict__ d2s) {
     const int NT = T * (T + 1) / 2;
     const int idx = xcd_tile(blockIdx.x, gridDim.x);
     const int g = idx / NT;
@@ -695,7 +751,9 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
         Pl = reinterpret_cast<const __bf16*>(reinterpret_cast<const char*>(Pl) + off);
         nrm = reinterpret_cast<const float*>(reinterpret_cast<const char*>(nrm) + off);
         D2 = reinterpret_cast<float*>(reinterpret_cast<char*>(D2) + off);
+        d2s = reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(d2s) + off);
     }
+    const float dsc = H ? d2_scale(*d2s) : 1.f;
     constexpr int kTP = 128 * kPK;                                  // bf16 per tile plane
     __shared__ __attribute__((aligned(16))) __bf16 sm[2 * 4 * kTP];  // 128 KiB: [buf][plane]
     const int lane = lane_id();
@@ -799,20 +857,19 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {   // direct: 32 lanes per 128-B row piece
                     const int i = i0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-                    if (i < n && j < n) D2[size_t(i) * ld + j] = dv[e];
+                    if (i < n && j < n) dput<H>(D2, size_t(i) * ld + j, dv[e], dsc);
                 }
                 if (j < n) {   // mirrored: row j, columns i0 + 8 g + 4 h .. +3
 #pragma unroll
                     for (int g = 0; g < 4; ++g) {
                         const int i = i0 + 8 * g + 4 * h;
-                        float* dst = D2 + size_t(j) * ld + i;
+                        const size_t o = size_t(j) * ld + i;
                         if (i + 4 <= n) {
-                            *reinterpret_cast<f32x4*>(dst) =
-                                f32x4{dv[4 * g], dv[4 * g + 1], dv[4 * g + 2], dv[4 * g + 3]};
+                            dput4<H>(D2, o, f32x4{dv[4 * g], dv[4 * g + 1], dv[4 * g + 2], dv[4 * g + 3]}, dsc);
                         } else {
 #pragma unroll
                             for (int t = 0; t < 4; ++t)
-                                if (i + t < n) dst[t] = dv[4 * g + t];
+                                if (i + t < n) dput<H>(D2, o + t, dv[4 * g + t], dsc);
                         }
                     }
                 }
@@ -836,7 +893,7 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
         for (int q = threadIdx.x; q < 128 * 128; q += 256) {
             const int ti = q >> 7, tj = q & 127;
             const int i = bi * 128 + ti, j = bi * 128 + tj;
-            if (i < n && j < n) D2[size_t(i) * ld + j] = tj >= ti ? tile[ti * 129 + tj] : tile[tj * 129 + ti];
+            if (i < n && j < n) dput<H>(D2, size_t(i) * ld + j, tj >= ti ? tile[ti * 129 + tj] : tile[tj * 129 + ti], dsc);
         }
     }
 }
@@ -867,12 +924,32 @@ __device__ __forceinline__ void list_pop(uint64_t (&key)[KC], bool pop) {
     key[KC - 1] = pop ? ~0ull : key[KC - 1];
 }
 
+// A row of D2 as the select reads it: fp32, or fp16 x s decoded x 1/s (H, the pre-split route;
+// 1/s is a power of two, so decoding adds no rounding).  Element offsets, 4-aligned for ld4.
+template <bool H>
+struct D2Row {
+    const char* base;
+    float inv;
+    __device__ __forceinline__ f32x4 ld4(size_t e) const {
+        if constexpr (H) {
+            const h16x4 v = *reinterpret_cast<const h16x4*>(base + 2 * e);
+            return f32x4{float(v.x) * inv, float(v.y) * inv, float(v.z) * inv, float(v.w) * inv};
+        } else {
+            return *reinterpret_cast<const f32x4*>(base + 4 * e);
+        }
+    }
+    __device__ __forceinline__ float ld1(size_t e) const {
+        if constexpr (H) return float(*reinterpret_cast<const _Float16*>(base + 2 * e)) * inv;
+        else return *reinterpret_cast<const float*>(base + 4 * e);
+    }
+};
+
 // Per-lane scan of row i of D2 (the sum of NP partial planes, added in plane order) into a
 // sorted list of the lane's KC smallest keys; returns how many valid columns the lane saw.
 // NB float4 per lane and plane are loaded before any is consumed (one memory latency per
 // 256*NB columns); addresses past the row are clamped, not branched around.
-template <int KC, int NP>
-__device__ __forceinline__ int scan_row(const float* __restrict__ row, size_t plane, int n,
+template <int KC, int NP, bool H = false>
+__device__ __forceinline__ int scan_row(const D2Row<H>& row, size_t plane, int n,
                                         int ld, int i, uint64_t (&key)[KC]) {
     constexpr int NB = 4;
     const int lane = lane_id();
@@ -885,9 +962,9 @@ __device__ __forceinline__ int scan_row(const float* __restrict__ row, size_t pl
         for (int b = 0; b < NB; ++b) {
             const int j0 = jb + 4 * (b * kWave + lane);
             const int jc = j0 < ld ? j0 : 0;
-            v[b] = *reinterpret_cast<const f32x4*>(row + jc);
+            v[b] = row.ld4(jc);
 #pragma unroll
-            for (int p = 1; p < NP; ++p) v[b] += *reinterpret_cast<const f32x4*>(row + p * plane + jc);
+            for (int p = 1; p < NP; ++p) v[b] += row.ld4(p * plane + jc);
         }
 #ifdef GLL_TRACE
         if (jb == 0) {
@@ -1062,8 +1139,8 @@ __device__ __forceinline__ bool merge_threshold(const uint64_t (&key)[KS], int k
 constexpr int kSelNB = 4;   // float4 per lane per 1024-column chunk of a D2 row
 
 // Loads of CH 1024-column chunks of D2 row `row` (sum of NP planes), clamped past ld.
-template <int NP, int CH>
-__device__ __forceinline__ void load_d2_row(const float* __restrict__ row, size_t plane, int ld,
+template <int NP, int CH, bool H = false>
+__device__ __forceinline__ void load_d2_row(const D2Row<H>& row, size_t plane, int ld,
                                             f32x4 (&v)[CH * kSelNB]) {
     const int lane = lane_id();
 #pragma unroll
@@ -1072,15 +1149,15 @@ __device__ __forceinline__ void load_d2_row(const float* __restrict__ row, size_
         for (int b = 0; b < kSelNB; ++b) {
             const int j0 = c * 4 * kWave * kSelNB + 4 * (b * kWave + lane);
             const int jc = j0 < ld ? j0 : 0;
-            v[c * kSelNB + b] = *reinterpret_cast<const f32x4*>(row + jc);
+            v[c * kSelNB + b] = row.ld4(jc);
 #pragma unroll
             for (int p = 1; p < NP; ++p)
-                v[c * kSelNB + b] += *reinterpret_cast<const f32x4*>(row + p * plane + jc);
+                v[c * kSelNB + b] += row.ld4(p * plane + jc);
         }
 }
 
-template <int TOP, int NP, int CH>
-__device__ __forceinline__ bool select_threshold(const float* __restrict__ row, size_t plane,
+template <int TOP, int NP, int CH, bool H = false>
+__device__ __forceinline__ bool select_threshold(const D2Row<H>& row, size_t plane,
                                                  int n, int ld, int i, int kc,
                                                  int* __restrict__ cand,
                                                  uint32_t* __restrict__ cgd, int& ci, int& kce,
@@ -1098,9 +1175,9 @@ __device__ __forceinline__ bool select_threshold(const float* __restrict__ row, 
         for (int b = 0; b < NB; ++b) {
             const int j0 = jb + 4 * (b * kWave + lane);
             const int jc = j0 < ld ? j0 : 0;
-            v[b] = *reinterpret_cast<const f32x4*>(row + jc);
+            v[b] = row.ld4(jc);
 #pragma unroll
-            for (int p = 1; p < NP; ++p) v[b] += *reinterpret_cast<const f32x4*>(row + p * plane + jc);
+            for (int p = 1; p < NP; ++p) v[b] += row.ld4(p * plane + jc);
         }
     };
     auto bits_of = [&](float x, int j) -> uint32_t {   // invalid: 0xFFFFFFFF (> any T)
@@ -1347,8 +1424,8 @@ struct KnnPick {
 // Exact rescan of every column with D2_gram <= thr (the certificate failed): candidates in
 // chunks of up to 64 - (K-1) lanes, float64 distances, the K-1 best (by d^2, index) carried
 // in lanes 0..K-2 across chunks (rare path, shallow load pipeline).
-template <bool VEC, int NP>
-__device__ __forceinline__ KnnPick knn_rescan(const float* __restrict__ row, size_t plane, int n,
+template <bool VEC, int NP, bool H = false>
+__device__ __forceinline__ KnnPick knn_rescan(const D2Row<H>& row, size_t plane, int n,
                                            int i, const float* __restrict__ X,
                                            const float* __restrict__ xi, int d, int K,
                                            double thr, int* s_cand) {
@@ -1360,9 +1437,9 @@ __device__ __forceinline__ KnnPick knn_rescan(const float* __restrict__ row, siz
         const int j = jb + lane;
         float v = 0.f;
         if (j < n) {
-            v = row[j];
+            v = row.ld1(j);
 #pragma unroll
-            for (int p = 1; p < NP; ++p) v += row[p * plane + j];
+            for (int p = 1; p < NP; ++p) v += row.ld1(p * plane + j);
         }
         bool take = j < n && j != i && v == v && double(v) <= thr;
         uint64_t mask = __ballot(take);
@@ -1403,7 +1480,8 @@ __device__ __forceinline__ KnnPick knn_rescan(const float* __restrict__ row, siz
 
 // XQ > 0: x_i staged in LDS, d <= 256 XQ.  CH > 0 (KC <= 32): n <= 1024 CH, the D2 row held in
 // registers by the threshold scan.
-template <int KC, bool VEC, int NP, int PG, int NU, int XQ = 0, bool R = false, int CH = 0>
+template <int KC, bool VEC, int NP, int PG, int NU, int XQ = 0, bool R = false, int CH = 0,
+          bool H = false>
 #ifndef GLL_SEL_WAVES
 #define GLL_SEL_WAVES 6
 #endif
@@ -1414,7 +1492,7 @@ void knn_select_kernel(
     float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ rev_cnt,
     int32_t* __restrict__ rev_idx, float* __restrict__ rev_d2, int32_t* __restrict__ ovf,
     int32_t* __restrict__ status, int32_t* __restrict__ status_pub, size_t xs, size_t wss,
-    size_t sts, int diag, int r0, int r1) {
+    size_t sts, int diag, int r0, int r1, const unsigned long long* __restrict__ d2s) {
     GLL_TRACE_SCOPE(1);
     GLL_TRACE_PT(20);
     const int2 gxy = batch_xy<R>();   // once (per pointer it re-reads gridDim and divides)
@@ -1429,6 +1507,7 @@ void knn_select_kernel(
     ovf = gshift_at(ovf, wss, gxy.y);
     status = gshift_at(status, wss, gxy.y);
     status_pub = gshift_at(status_pub, sts, gxy.y);
+    d2s = gshift_at(d2s, wss, gxy.y);
     __shared__ int s_cand[4][kWave];
     __shared__ uint32_t s_cgd[4][kWave];
     constexpr bool XL = XQ > 0;
@@ -1452,7 +1531,16 @@ void knn_select_kernel(
 
     // 1-2) candidates: short per-lane lists + threshold merge, exact re-run when inexact.
     //      tb: D2 bits every non-candidate column is >= to (+inf: all valid columns taken)
-    const float* row = D2 + size_t(i - r0) * ld;
+    // fp16 storage (H): decoded x 1/s; its rounding widens every Gram error bound below by
+    // rho (relative, half an fp16 ulp) plus sub (absolute, half the smallest subnormal step)
+    const float dsc = H ? d2_scale(*d2s) : 1.f;
+    const D2Row<H> row{reinterpret_cast<const char*>(D2) + size_t(i - r0) * ld * (H ? 2 : 4),
+                       1.f / dsc};
+    const double rho = H ? 1.0 / 2048.0 : 0.0;
+    const double sub = H ? 0x1p-25 / double(dsc) : 0.0;
+    // bounds between a true Gram value v and its stored decoding t: |t - v| <= rho |v| + sub
+    auto up = [&](double t) { return H ? t + 2.0 * rho * fabs(t) + sub : t; };   // >= v
+    auto lo = [&](double t) { return H ? t - 2.0 * rho * fabs(t) - sub : t; };   // <= v
     constexpr int KS = KC <= 16 ? 4 : 8;
     int ci, kce;
     uint32_t tb, gb;   // gb: this lane's candidate's Gram D2 bits
@@ -1460,8 +1548,8 @@ void knn_select_kernel(
         bool redo;
         if constexpr (KC <= 32) {
             f32x4 vrow[CH > 0 ? CH * kSelNB : 1];
-            if constexpr (CH > 0) load_d2_row<NP, CH>(row, plane, ld, vrow);
-            redo = select_threshold<KC == 16 ? 2 : 3, NP, CH>(row, plane, n, ld, i, kc, s_cand[wv],
+            if constexpr (CH > 0) load_d2_row<NP, CH, H>(row, plane, ld, vrow);
+            redo = select_threshold<KC == 16 ? 2 : 3, NP, CH, H>(row, plane, n, ld, i, kc, s_cand[wv],
                                                               s_cgd[wv], ci, kce, tb, gb, vrow);
             if constexpr (XL) {
 #pragma unroll
@@ -1470,7 +1558,7 @@ void knn_select_kernel(
             }
         } else {
             uint64_t key[KS];
-            const int seen = scan_row<KS, NP>(row, plane, n, ld, i, key);
+            const int seen = scan_row<KS, NP, H>(row, plane, n, ld, i, key);
             GLL_TRACE_PT(16);
             if constexpr (XL) {
 #pragma unroll
@@ -1483,7 +1571,7 @@ void knn_select_kernel(
         if (redo) {
             if (lane == 0) atomicAdd(&status_pub[GLL_ST_KNN_MERGE], 1);
             uint64_t full[KC];
-            scan_row<KC, NP>(row, plane, n, ld, i, full);
+            scan_row<KC, NP, H>(row, plane, n, ld, i, full);
             ci = merge_exact<KC>(full, kc, tb, gb);
             kce = kc;
         }
@@ -1512,15 +1600,15 @@ void knn_select_kernel(
         }
         const uint64_t kb = __ballot(lane < kce && ci >= 0 && grk == K - 2);
         if (kb) {
-            const double G = double(readlane_f(g, int(__builtin_ctzll(kb))));
-            float a2 = row[0];
+            const double G = up(double(readlane_f(g, int(__builtin_ctzll(kb)))));
+            float a2 = row.ld1(0);
 #pragma unroll
-            for (int p = 1; p < NP; ++p) a2 += row[p * plane];
-            const double ai = sqrt(double(a2 > 0.f ? a2 : 0.f));
+            for (int p = 1; p < NP; ++p) a2 += row.ld1(p * plane);
+            const double ai = sqrt(up(double(a2 > 0.f ? a2 : 0.f)));
             const double gp = G > 0.0 ? G : 0.0;
             const double b0 = kGramErr * (2.0 * ai + sqrt(gp)) * (2.0 * ai + sqrt(gp));
             const double r1 = 2.0 * ai + sqrt(gp + b0);
-            const double thr = G + 2.0 * kGramErr * r1 * r1;
+            const double thr = up(G + 2.0 * kGramErr * r1 * r1);   // in stored units
             const bool need = lane < kce && ci >= 0 && (grk < K - 1 || double(g) <= thr);
             const bool drop = lane < kce && ci >= 0 && !need;
             // the smallest dropped Gram D2 joins the left-out bound
@@ -1589,15 +1677,16 @@ void knn_select_kernel(
     if (K >= 2 && nkeep == K - 1 && tb < 0x7F800000u) {
         const uint64_t kb = __ballot(keep && rank == K - 2);
         const double dK = readlane_d(ce, int(__builtin_ctzll(kb)));
-        float a2 = row[0];
+        float a2 = row.ld1(0);
 #pragma unroll
-        for (int p = 1; p < NP; ++p) a2 += row[p * plane];
-        const double ai = sqrt(double(a2 > 0.f ? a2 : 0.f));
+        for (int p = 1; p < NP; ++p) a2 += row.ld1(p * plane);
+        const double ai = sqrt(up(double(a2 > 0.f ? a2 : 0.f)));
         const double r = 2.0 * ai + sqrt(dK);
         const double thr = dK + kGramErr * r * r;
-        if (!(double(__uint_as_float(tb)) > thr)) {
+        if (!(lo(double(__uint_as_float(tb))) > thr)) {
             if (lane == 0) atomicAdd(&status_pub[GLL_ST_KNN_RESCAN], 1);
-            const KnnPick pk = knn_rescan<VEC, NP>(row, plane, n, i, X, xi, d, K, thr, s_cand[wv]);
+            const KnnPick pk = knn_rescan<VEC, NP, H>(row, plane, n, i, X, xi, d, K, up(thr),
+                                                      s_cand[wv]);
             ci = pk.j;
             ce = pk.d;
             kce = K - 1;
@@ -1665,11 +1754,13 @@ void knn_select_kernel(
 // --------------------------------------------------------------------------------------
 constexpr int kPK2 = 32;   // features per k-stage of the 256-tile kernel
 
+template <bool H>
 __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict__ Ph,
                                                        const __bf16* __restrict__ Pl,
                                                        const float* __restrict__ nrm, int n,
                                                        int dp, int T, float* __restrict__ D2,
-                                                       int ld, size_t wss, int diag_epi) {
+                                                       int ld, size_t wss, int diag_epi,
+                                                       const unsigned long long* __restrict__ d2s) {
     const int NT = T * (T + 1) / 2;
     const int idx = xcd_tile(blockIdx.x, gridDim.x);
     const int g = idx / NT;
@@ -1679,7 +1770,9 @@ __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict_
         Pl = reinterpret_cast<const __bf16*>(reinterpret_cast<const char*>(Pl) + off);
         nrm = reinterpret_cast<const float*>(reinterpret_cast<const char*>(nrm) + off);
         D2 = reinterpret_cast<float*>(reinterpret_cast<char*>(D2) + off);
+        d2s = reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(d2s) + off);
     }
+    const float dsc = H ? d2_scale(*d2s) : 1.f;
     constexpr int kTP = 256 * kPK2;                                 // bf16 per tile plane
     constexpr int kSS = 260;   // epilogue staging: 128 rows x 256 columns, row stride 260 floats
     constexpr int kSM = 2 * 4 * kTP > 2 * 128 * kSS ? 2 * 4 * kTP : 2 * 128 * kSS;
@@ -1792,14 +1885,14 @@ __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict_
 #pragma unroll
                     for (int gq = 0; gq < 4; ++gq) {
                         const int i = i0 + 8 * gq + 4 * h;
-                        float* dst = D2 + size_t(j) * ld + i;
+                        const size_t o = size_t(j) * ld + i;
                         if (i + 4 <= n) {
-                            *reinterpret_cast<f32x4*>(dst) = f32x4{acc[a][b][4 * gq],
-                                acc[a][b][4 * gq + 1], acc[a][b][4 * gq + 2], acc[a][b][4 * gq + 3]};
+                            dput4<H>(D2, o, f32x4{acc[a][b][4 * gq], acc[a][b][4 * gq + 1],
+                                                  acc[a][b][4 * gq + 2], acc[a][b][4 * gq + 3]}, dsc);
                         } else {
 #pragma unroll
                             for (int t = 0; t < 4; ++t)
-                                if (i + t < n) dst[t] = acc[a][b][4 * gq + t];
+                                if (i + t < n) dput<H>(D2, o + t, acc[a][b][4 * gq + t], dsc);
                         }
                     }
                 }
@@ -1828,13 +1921,13 @@ __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict_
                 const int i = bi * 256 + hh * 128 + row;
                 const f32x4 v = *reinterpret_cast<const f32x4*>(stg + row * kSS + 4 * lane);
                 if (i < n) {
-                    float* dst = D2 + size_t(i) * ld + j;
+                    const size_t o = size_t(i) * ld + j;
                     if (j + 4 <= n) {
-                        *reinterpret_cast<f32x4*>(dst) = v;
+                        dput4<H>(D2, o, v, dsc);
                     } else {
 #pragma unroll
                         for (int t = 0; t < 4; ++t)
-                            if (j + t < n) dst[t] = v[t];
+                            if (j + t < n) dput<H>(D2, o + t, v[t], dsc);
                     }
                 }
             }
@@ -1864,21 +1957,20 @@ __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict_
             for (int e = 0; e < 16; ++e) {   // direct: 32 lanes per 128-B row piece
                 const int ti = ti0 + (e & 3) + 8 * (e >> 2) + 4 * h;
                 const int i = bi * 256 + ti;
-                if (i < n && j < n && (!diag || tj >= ti)) D2[size_t(i) * ld + j] = dv[e];
+                if (i < n && j < n && (!diag || tj >= ti)) dput<H>(D2, size_t(i) * ld + j, dv[e], dsc);
             }
             if (j < n) {   // mirrored: row j, columns i0 + 8 g + 4 h .. +3
 #pragma unroll
                 for (int gq = 0; gq < 4; ++gq) {
                     const int ti = ti0 + 8 * gq + 4 * h;
                     const int i = bi * 256 + ti;
-                    float* dst = D2 + size_t(j) * ld + i;
+                    const size_t o = size_t(j) * ld + i;
                     if (i + 4 <= n && (!diag || tj >= ti + 3)) {
-                        *reinterpret_cast<f32x4*>(dst) =
-                            f32x4{dv[4 * gq], dv[4 * gq + 1], dv[4 * gq + 2], dv[4 * gq + 3]};
+                        dput4<H>(D2, o, f32x4{dv[4 * gq], dv[4 * gq + 1], dv[4 * gq + 2], dv[4 * gq + 3]}, dsc);
                     } else {
 #pragma unroll
                         for (int t = 0; t < 4; ++t)
-                            if (i + t < n && (!diag || tj >= ti + t)) dst[t] = dv[4 * gq + t];
+                            if (i + t < n && (!diag || tj >= ti + t)) dput<H>(D2, o + t, dv[4 * gq + t], dsc);
                     }
                 }
             }
@@ -1905,6 +1997,19 @@ static bool gram_tile256(const Layout& L, const Batch& bt, int T, int T2) {
     const int64_t t1 = int64_t(bt.B) * T * (T + 1) / 2, t2 = int64_t(bt.B) * T2 * (T2 + 1) / 2;
     const int64_t r1 = (t1 + cus - 1) / cus, r2 = (t2 + cus - 1) / cus;
     return r2 * 2 * (L.dp / kPK2) * kPK2 < r1 * (L.dp / kPK) * kPK;   // stage bytes equal
+}
+
+// The pre-split route (gram_split + gram_pk / gram_pk2): batches, and single graphs with d > 128
+// and n <= 12,288 (see launch_gram).  Its D2 is stored fp16 (dput) unless GLL_D2_F32 = 1 (A/B).
+static bool presplit_route(const Layout& L, const Batch& bt) {
+    const int T = (L.n + 127) / 128;
+    return !(L.flags & GLL_FLAG_GRAM_NARROW) && int64_t(bt.B) * T * (T + 1) / 2 >= 256 &&
+           !(L.flags & GLL_FLAG_GRAM_INLINE) && (bt.B > 1 || (L.d > 128 && L.n <= 12288)) &&
+           gram_planes(L, bt.B) == 1 && L.PR == L.n;
+}
+static bool d2_half(const Layout& L, const Batch& bt) {
+    static const bool f32 = getenv("GLL_D2_F32") && atoi(getenv("GLL_D2_F32")) != 0;
+    return !f32 && !(L.flags & GLL_FLAG_D2_F32) && presplit_route(L, bt);
 }
 
 hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
@@ -1937,8 +2042,7 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
     // 8.7 ms at 30,250 x 512, 17.5 vs 11.4 ms at 30,250 x 1024 (tools/gram_route_probe.py,
     // profiles/r02j_gram_route.txt); the stress shape (8,192 x 1024) is the largest measured where
     // it wins, and the 12,288 cut between the two is not measured.
-    if (!(L.flags & GLL_FLAG_GRAM_NARROW) && int64_t(bt.B) * T * (T + 1) / 2 >= 256 &&
-        !(L.flags & GLL_FLAG_GRAM_INLINE) && (bt.B > 1 || (L.d > 128 && L.n <= 12288))) {
+    if (presplit_route(L, bt)) {
         // split once (one pass over X), then the LDS-DMA bf16 GEMM over 128-tiles
         __bf16* Ph = L.at<__bf16>(ws, L.xhi);
         __bf16* Pl = L.at<__bf16>(ws, L.xlo);
@@ -1946,18 +2050,24 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         prof_begin(GLL_K_GRAM, s);
         prof_span(2);
         const dim3 sgrid((L.n + 3) / 4, bt.B);
+        static std::atomic<unsigned long long> gen_ctr{0};
+        const unsigned long long gen = (++gen_ctr) & ((1ull << 40) - 1);   // 40-bit call tag
+        auto* d2s = L.at<unsigned long long>(ws, L.d2s);
         if (vec)
-            launch_k(gram_split_kernel<true>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
+            launch_k(gram_split_kernel<true>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws, d2s, gen);
         else
-            launch_k(gram_split_kernel<false>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
+            launch_k(gram_split_kernel<false>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws, d2s, gen);
+        const bool H = d2_half(L, bt);
         const int T2 = (L.n + 255) / 256;
         static const int gram_diag = getenv("GLL_GRAM_DIAG") ? atoi(getenv("GLL_GRAM_DIAG")) : 0;
         if (gram_tile256(L, bt, T, T2))
-            launch_k(gram_pk2_kernel, dim3(unsigned(bt.B * T2 * (T2 + 1) / 2)), 512, 0, s, Ph,
-                     Pl, nrm, L.n, L.dp, T2, D2, L.ldD, bt.ws, gram_diag);
+            launch_k(H ? gram_pk2_kernel<true> : gram_pk2_kernel<false>,
+                     dim3(unsigned(bt.B * T2 * (T2 + 1) / 2)), 512, 0, s, Ph, Pl, nrm, L.n, L.dp,
+                     T2, D2, L.ldD, bt.ws, gram_diag, d2s);
         else
-            launch_k(gram_pk_kernel, dim3(unsigned(bt.B * T * (T + 1) / 2)), 256, 0, s, Ph, Pl,
-                     nrm, L.n, L.dp, T, D2, L.ldD, bt.ws);
+            launch_k(H ? gram_pk_kernel<true> : gram_pk_kernel<false>,
+                     dim3(unsigned(bt.B * T * (T + 1) / 2)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T,
+                     D2, L.ldD, bt.ws, d2s);
         prof_end(GLL_K_GRAM, s);
         return launch_status("knn.hip:launch_gram(pk)");
     }
@@ -2022,6 +2132,8 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     const size_t plane = size_t(n) * L.ldD;
     const int planes = gram_planes(L, bt.B);
     dim3 grid((rows + 3) / 4, bt.B);
+    const bool h16 = planes == 1 && d2_half(L, bt);   // the Gram stored D2 as fp16 x s
+    const auto* d2s = L.at<unsigned long long>(ws, L.d2s);
     prof_begin(GLL_K_SELECT, s);
 // Batched launches (PG = 1) stage x_i in LDS (XQ quarters of 256 features, d <= 1024) and run at
 // 6 waves per SIMD: measured at B = 64 NS, select 259 -> 214 us (XQ = 2, NU = 8; the NU = 16
@@ -2031,15 +2143,20 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
 // Batched launches number blocks XCD-contiguously (R = true: each XCD works through a run of
 // graphs): NS B = 64 220 -> 213 us, FullySup B = 64 440 -> 429 us (profiles/r02h_xcd_ab.txt),
 // once the kernel took its graph index once instead of per pointer.
-#define GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, CHV)                                              \
-    launch_k((bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2, NUS, 0, false, CHV>                \
-                        : knn_select_kernel<KCV, V, NPV, 1, NUB, (V ? XQV : 0), true, CHV>), grid, 256, 0, s, \
+#define GLL_SEL6(KCV, V, NPV, NUS, NUB, XQV, CHV, HV)                                          \
+    launch_k((bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2, NUS, 0, false, CHV, HV>            \
+                        : knn_select_kernel<KCV, V, NPV, 1, NUB, (V ? XQV : 0), true, CHV, HV>), grid, 256, 0, s, \
         L.at<float>(ws, L.D2), L.ldD, plane, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0,     \
         L.RCAP,                                                                                \
         L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \
         L.at<int32_t>(ws, L.rev_cnt), L.at<int32_t>(ws, L.rev_idx), L.at<float>(ws, L.rev_d2), \
         L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub, bt.x, bt.ws, bt.st, diag, \
-        r0, r0 + rows)
+        r0, r0 + rows, d2s)
+#define GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, CHV)                                              \
+    do {                                                                                       \
+        if (h16) GLL_SEL6(KCV, V, NPV, NUS, NUB, XQV, CHV, (NPV == 1));                        \
+        else GLL_SEL6(KCV, V, NPV, NUS, NUB, XQV, CHV, false);                                 \
+    } while (0)
 // the threshold scan holds rows of <= 2048 columns in registers (KC <= 32, aligned d)
 #define GLL_SEL4(KCV, V, NPV, NUS, NUB, XQV)                                                   \
     do {                                                                                       \
@@ -2062,6 +2179,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
 #undef GLL_SEL
 #undef GLL_SEL4
 #undef GLL_SEL5
+#undef GLL_SEL6
     prof_end(GLL_K_SELECT, s);
     return launch_status("knn.hip:launch_select");
 }

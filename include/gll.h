@@ -77,6 +77,9 @@ extern "C" {
                                     * (diagnostic) */
 #define GLL_FLAG_CG_PAIRS 32768    /* batched per-column CG: two right-hand-side columns per
                                     * workgroup (measured slower; diagnostic) */
+#define GLL_FLAG_D2_F32 131072     /* pre-split Gram route (batches, mid-size graphs with d > 128):
+                                    * keep the distance matrix fp32 instead of fp16 x 2^e
+                                    * (diagnostic) */
 #define GLL_FLAG_KNN_PANEL 65536   /* single graphs: build the kNN in row panels of 1,024 rows
                                     * (an O(panel x n) distance buffer instead of n x n; automatic
                                     * past 32 GiB of n x n distances, panels of 8 GiB) */
