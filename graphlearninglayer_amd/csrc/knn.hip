@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include <atomic>
+#include <chrono>
 
 #include "gll_internal.h"
 
@@ -690,11 +691,22 @@ __global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict
         s_key[threadIdx.x >> 6] = (b + 0xFFu) >> 8;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {   // the graph's max |a|^2 for the fp16 D2 scale, tagged with the
-        unsigned k = s_key[0];  // call's generation so an earlier call's word never wins
+    if (threadIdx.x == 0) {
+        // the graph's max |a|^2 for the fp16 D2 scale, tagged with this call's generation: a
+        // word with another tag (an earlier call's, or whatever the workspace held) is
+        // replaced, one with this tag only raised -- no reset needed, uninitialised memory
+        // included (generations start at a random 40-bit value per process)
+        unsigned k = s_key[0];
 #pragma unroll
         for (int q = 1; q < 4; ++q) k = s_key[q] > k ? s_key[q] : k;
-        atomicMax(d2s, (gen << 24) | (unsigned long long)k);
+        const unsigned long long want = (gen << 24) | (unsigned long long)k;
+        unsigned long long old = __hip_atomic_load(d2s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int guard = 0; guard < 1 << 20; ++guard) {
+            if ((old >> 24) == gen && (old & 0xFFFFFFull) >= k) break;
+            const unsigned long long prev = atomicCAS(d2s, old, want);
+            if (prev == old) break;
+            old = prev;
+        }
     }
 }
 
@@ -2007,9 +2019,12 @@ static bool presplit_route(const Layout& L, const Batch& bt) {
            !(L.flags & GLL_FLAG_GRAM_INLINE) && (bt.B > 1 || (L.d > 128 && L.n <= 12288)) &&
            gram_planes(L, bt.B) == 1 && L.PR == L.n;
 }
+// Batches only (GLL_D2_HALF1 = 1 extends it to single graphs for A/B): see DESIGN.md §3.1 and
+// profiles/r03x_d2_fp16_ab.txt.
 static bool d2_half(const Layout& L, const Batch& bt) {
     static const bool f32 = getenv("GLL_D2_F32") && atoi(getenv("GLL_D2_F32")) != 0;
-    return !f32 && !(L.flags & GLL_FLAG_D2_F32) && presplit_route(L, bt);
+    static const bool one = getenv("GLL_D2_HALF1") && atoi(getenv("GLL_D2_HALF1")) != 0;  // A/B
+    return !f32 && !(L.flags & GLL_FLAG_D2_F32) && (bt.B > 1 || one) && presplit_route(L, bt);
 }
 
 hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
@@ -2050,8 +2065,11 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         prof_begin(GLL_K_GRAM, s);
         prof_span(2);
         const dim3 sgrid((L.n + 3) / 4, bt.B);
-        static std::atomic<unsigned long long> gen_ctr{0};
-        const unsigned long long gen = (++gen_ctr) & ((1ull << 40) - 1);   // 40-bit call tag
+        // 40-bit call tag: a random start per process, then one step per call
+        static std::atomic<unsigned long long> gen_ctr{
+            (std::chrono::steady_clock::now().time_since_epoch().count() * 0x9E3779B97F4A7C15ull) ^
+            (unsigned long long)(uintptr_t)&gen_ctr};
+        const unsigned long long gen = (++gen_ctr) & ((1ull << 40) - 1);
         auto* d2s = L.at<unsigned long long>(ws, L.d2s);
         if (vec)
             launch_k(gram_split_kernel<true>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws, d2s, gen);

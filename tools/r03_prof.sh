@@ -16,6 +16,7 @@ for cfg in ns stress fullysup; do
   steps+=("${T}_prof_${cfg}:150:$P $ST_ARGS -d gpurun_out/${T}_prof_${cfg} -o run -- $C")
 done
 steps+=("${T}_prof_b64:150:PROBE_B=64 $P $ST_ARGS -d gpurun_out/${T}_prof_b64 -o run -- python3 $R/tools/batch_probe.py")
+steps+=("${T}_prof_fs_b64:150:PROBE_B=64 PROBE_CFG=fullysup $P $ST_ARGS -d gpurun_out/${T}_prof_fs_b64 -o run -- python3 $R/tools/batch_probe.py")
 for cfg in ns stress; do
   case $cfg in ns) C="$NS";; stress) C="$ST";; esac
   steps+=("${T}_pmcf_${cfg}:120:$P --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/${T}_pmcf_${cfg} -o run -- $C")
