@@ -178,7 +178,7 @@ struct Layout {
     int dp;           // split-Gram planes: d rounded up to 64
     size_t xhi, xlo, xnrm;   // [n][dp] bf16 hi / lo planes of x - x_0, and |x - x_0|^2
     size_t fsync;     // fused backward: [0] solved columns, [32] finished gradient blocks
-    size_t d2s;       // u64: (call generation << 24) | max |a|^2 bits, the fp16 D2 scale
+    size_t d2s;       // float: the fp16 D2 scale of the pre-split GEMM (knn.hip tile_d2_scale)
 
     explicit Layout(const gll_problem& p) {
         n = p.n; d = p.d; base = p.base; C = p.C;
@@ -228,7 +228,7 @@ struct Layout {
         xlo = take(size_t(n) * dp * 2);
         xnrm = take(size_t(n) * 4);
         fsync = take(256);   // two counters on their own 128-B lines, zeroed by row_build
-        d2s = take(256);     // fp16 D2 scale word of the pre-split Gram (knn.hip gram_split)
+        d2s = take(256);     // fp16 D2 scale of the pre-split Gram (knn.hip tile_d2_scale)
         P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)
         Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
         S = take(size_t(Etot) * 4);        // per-edge coefficient (auto eps / chunked gradient)

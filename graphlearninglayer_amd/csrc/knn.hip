@@ -27,8 +27,6 @@
 
 #include <type_traits>
 
-#include <atomic>
-#include <chrono>
 
 #include "gll_internal.h"
 
@@ -625,16 +623,33 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
 constexpr int kPK = 64;                  // features per k-stage
 typedef __attribute__((address_space(3))) void lds_void;
 
-// fp16 D2 scale of a graph from its gram_split word: s = 2^(14 - e) with 4 max|a|^2 < 2^e, so
-// every stored D2 x s stays below 2^14 (fp16 max 65504); 1 for an all-zero or non-finite graph.
-__device__ __forceinline__ float d2_scale(unsigned long long w) {
-    const float t = 4.f * __uint_as_float(uint32_t(w & 0xFFFFFFull) << 8);
+// fp16 D2 scale of a graph with M = max |a_i|^2: s = 2^(14 - e) with 4M < 2^e, so every
+// stored D2 x s stays below 2^14 (fp16 max 65504); 1 for an all-zero or non-finite graph.
+__device__ __forceinline__ float d2_scale(float M) {
+    const float t = 4.f * M;
     if (!(t > 1e-30f) || !(t < 1e38f)) return 1.f;
     int e;
     (void)frexpf(t, &e);   // t = f 2^e, f in [0.5, 1)
     int k = 14 - e;
     k = k < -120 ? -120 : (k > 120 ? 120 : k);
     return ldexpf(1.f, k);
+}
+
+// Block-wide max of nrm[0 .. n) (the graph's |a_i|^2 from gram_split) -> the fp16 scale; every
+// tile of the GEMM computes the same value from the same array, and each stores it to the
+// graph's scale word for the select: identical plain stores, no atomics, nothing to reset.
+template <int NT>
+__device__ __forceinline__ float tile_d2_scale(const float* __restrict__ nrm, int n, float* red) {
+    float mx = 0.f;
+    for (int q = threadIdx.x; q < n; q += NT) mx = fmaxf(mx, nrm[q]);   // NaN: dropped
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    mx = 0.f;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) mx = fmaxf(mx, red[w]);
+    return d2_scale(mx);
 }
 
 template <bool VEC>
@@ -644,11 +659,8 @@ __global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict
                                                          float* __restrict__ nrm,
                                                          int32_t* __restrict__ status,
                                                          int32_t* __restrict__ rev_cnt,
-                                                         size_t xs, size_t wss,
-                                                         unsigned long long* __restrict__ d2s,
-                                                         unsigned long long gen) {
+                                                         size_t xs, size_t wss) {
     X = gshift_br(X, xs);
-    d2s = gshift_br(d2s, wss);
     Ph = gshift_br(Ph, wss);
     Pl = gshift_br(Pl, wss);
     nrm = gshift_br(nrm, wss);
@@ -661,12 +673,7 @@ __global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict
     }
     const int lane = lane_id();
     const int i = bx() * 4 + (threadIdx.x >> 6);
-    __shared__ unsigned s_key[4];
-    if (i >= n) {
-        if (lane == 0) s_key[threadIdx.x >> 6] = 0u;
-        __syncthreads();
-        return;
-    }
+    if (i >= n) return;
     const float* xi = X + size_t(i) * d;
     float sq = 0.f;
     for (int k = 4 * lane; k < dp; k += 4 * kWave) {
@@ -684,30 +691,7 @@ __global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict
         *reinterpret_cast<bf16x4*>(Pl + size_t(i) * dp + k) = lv;
     }
     sq = wave_sum_dpp(sq);
-    if (lane == 0) {
-        nrm[i] = sq;
-        // |a_i|^2 rounded up to 24 bits of its float pattern (>= the value; NaN orders last)
-        const uint32_t b = __float_as_uint(sq > 0.f ? sq : 0.f) & 0x7FFFFFFFu;
-        s_key[threadIdx.x >> 6] = (b + 0xFFu) >> 8;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        // the graph's max |a|^2 for the fp16 D2 scale, tagged with this call's generation: a
-        // word with another tag (an earlier call's, or whatever the workspace held) is
-        // replaced, one with this tag only raised -- no reset needed, uninitialised memory
-        // included (generations start at a random 40-bit value per process)
-        unsigned k = s_key[0];
-#pragma unroll
-        for (int q = 1; q < 4; ++q) k = s_key[q] > k ? s_key[q] : k;
-        const unsigned long long want = (gen << 24) | (unsigned long long)k;
-        unsigned long long old = __hip_atomic_load(d2s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int guard = 0; guard < 1 << 20; ++guard) {
-            if ((old >> 24) == gen && (old & 0xFFFFFFull) >= k) break;
-            const unsigned long long prev = atomicCAS(d2s, old, want);
-            if (prev == old) break;
-            old = prev;
-        }
-    }
+    if (lane == 0) nrm[i] = sq;
 }
 
 // Tile t of the upper triangle of T x T blocks in supertile order: supertiles of kSR x kSC
@@ -753,7 +737,7 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
                                                       const float* __restrict__ nrm, int n,
                                                       int dp, int T, float* __restrict__ D2,
                                                       int ld, size_t wss,
-                                                      const unsigned long long* __restrict__ d2s) {
+                                                      float* __restrict__ d2s) {
     const int NT = T * (T + 1) / 2;
     const int idx = xcd_tile(blockIdx.x, gridDim.x);
     const int g = idx / NT;
@@ -763,9 +747,8 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
         Pl = reinterpret_cast<const __bf16*>(reinterpret_cast<const char*>(Pl) + off);
         nrm = reinterpret_cast<const float*>(reinterpret_cast<const char*>(nrm) + off);
         D2 = reinterpret_cast<float*>(reinterpret_cast<char*>(D2) + off);
-        d2s = reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(d2s) + off);
+        d2s = reinterpret_cast<float*>(reinterpret_cast<char*>(d2s) + off);
     }
-    const float dsc = H ? d2_scale(*d2s) : 1.f;
     constexpr int kTP = 128 * kPK;                                  // bf16 per tile plane
     __shared__ __attribute__((aligned(16))) __bf16 sm[2 * 4 * kTP];  // 128 KiB: [buf][plane]
     const int lane = lane_id();
@@ -815,6 +798,12 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
     // before those DMAs are issued.
 #pragma unroll
     for (int q0 = 0; q0 < 16; q0 += 4) issue4(0, 0, q0);
+    float dsc = 1.f;   // fp16 D2 scale (H), computed under the first stage's DMAs
+    if constexpr (H) {
+        __shared__ float red[4];
+        dsc = tile_d2_scale<256>(nrm, n, red);
+        if (threadIdx.x == 0) *d2s = dsc;
+    }
     for (int ks = 0; ks < nks; ++ks) {
         const int buf = ks & 1;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's stage-ks DMAs
@@ -1504,7 +1493,7 @@ void knn_select_kernel(
     float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ rev_cnt,
     int32_t* __restrict__ rev_idx, float* __restrict__ rev_d2, int32_t* __restrict__ ovf,
     int32_t* __restrict__ status, int32_t* __restrict__ status_pub, size_t xs, size_t wss,
-    size_t sts, int diag, int r0, int r1, const unsigned long long* __restrict__ d2s) {
+    size_t sts, int diag, int r0, int r1, const float* __restrict__ d2s) {
     GLL_TRACE_SCOPE(1);
     GLL_TRACE_PT(20);
     const int2 gxy = batch_xy<R>();   // once (per pointer it re-reads gridDim and divides)
@@ -1545,7 +1534,7 @@ void knn_select_kernel(
     //      tb: D2 bits every non-candidate column is >= to (+inf: all valid columns taken)
     // fp16 storage (H): decoded x 1/s; its rounding widens every Gram error bound below by
     // rho (relative, half an fp16 ulp) plus sub (absolute, half the smallest subnormal step)
-    const float dsc = H ? d2_scale(*d2s) : 1.f;
+    const float dsc = H ? *d2s : 1.f;   // written by every tile of the GEMM (the same value)
     const D2Row<H> row{reinterpret_cast<const char*>(D2) + size_t(i - r0) * ld * (H ? 2 : 4),
                        1.f / dsc};
     const double rho = H ? 1.0 / 2048.0 : 0.0;
@@ -1766,13 +1755,13 @@ void knn_select_kernel(
 // --------------------------------------------------------------------------------------
 constexpr int kPK2 = 32;   // features per k-stage of the 256-tile kernel
 
-template <bool H>
+template <bool H, bool PIPE>
 __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict__ Ph,
                                                        const __bf16* __restrict__ Pl,
                                                        const float* __restrict__ nrm, int n,
                                                        int dp, int T, float* __restrict__ D2,
                                                        int ld, size_t wss, int diag_epi,
-                                                       const unsigned long long* __restrict__ d2s) {
+                                                       float* __restrict__ d2s) {
     const int NT = T * (T + 1) / 2;
     const int idx = xcd_tile(blockIdx.x, gridDim.x);
     const int g = idx / NT;
@@ -1782,9 +1771,8 @@ __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict_
         Pl = reinterpret_cast<const __bf16*>(reinterpret_cast<const char*>(Pl) + off);
         nrm = reinterpret_cast<const float*>(reinterpret_cast<const char*>(nrm) + off);
         D2 = reinterpret_cast<float*>(reinterpret_cast<char*>(D2) + off);
-        d2s = reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(d2s) + off);
+        d2s = reinterpret_cast<float*>(reinterpret_cast<char*>(d2s) + off);
     }
-    const float dsc = H ? d2_scale(*d2s) : 1.f;
     constexpr int kTP = 256 * kPK2;                                 // bf16 per tile plane
     constexpr int kSS = 260;   // epilogue staging: 128 rows x 256 columns, row stride 260 floats
     constexpr int kSM = 2 * 4 * kTP > 2 * 128 * kSS ? 2 * 4 * kTP : 2 * 128 * kSS;
@@ -1830,38 +1818,78 @@ __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict_
     const int nks = dp / kPK2;
     issue4(0, 0, 0);
     issue4(0, 0, 4);
-    for (int ks = 0; ks < nks; ++ks) {
-        const int buf = ks & 1;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's stage-ks DMAs
-        __builtin_amdgcn_s_barrier();                          // every wave's
-        const bool more = ks + 1 < nks;
+    float dsc = 1.f;   // fp16 D2 scale (H), computed under the first stage's DMAs
+    if constexpr (H) {
+        __shared__ float red[8];
+        dsc = tile_d2_scale<512>(nrm, n, red);
+        if (threadIdx.x == 0) *d2s = dsc;
+    }
+    if constexpr (PIPE) {
+        // both k-steps' fragments of a stage requested at once (two register sets), so the
+        // second set's LDS reads run under the first set's 24 MFMAs (GLL_GRAM_PIPE, A/B)
+        for (int ks = 0; ks < nks; ++ks) {
+            const int buf = ks & 1;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            const bool more = ks + 1 < nks;
+            bf16x8 ah[2][2], al[2][2], bh[2][4], bl[2][4];
 #pragma unroll
-        for (int kk = 0; kk < kPK2 / 16; ++kk) {
-            if (more) issue4(ks + 1, buf ^ 1, 4 * kk);
-            bf16x8 ah[2], al[2], bh[4], bl[4];
+            for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                ah[m] = frag(buf, 0, wr * 64 + m * 32 + r, kk);
-                al[m] = frag(buf, 1, wr * 64 + m * 32 + r, kk);
-            }
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                bh[m] = frag(buf, 2, wc * 128 + m * 32 + r, kk);
-                bl[m] = frag(buf, 3, wc * 128 + m * 32 + r, kk);
-            }
-#pragma unroll
-            for (int a = 0; a < 2; ++a)
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+                for (int m = 0; m < 2; ++m) {
+                    ah[kk][m] = frag(buf, 0, wr * 64 + m * 32 + r, kk);
+                    al[kk][m] = frag(buf, 1, wr * 64 + m * 32 + r, kk);
                 }
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    bh[kk][m] = frag(buf, 2, wc * 128 + m * 32 + r, kk);
+                    bl[kk][m] = frag(buf, 3, wc * 128 + m * 32 + r, kk);
+                }
+            }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                if (more) issue4(ks + 1, buf ^ 1, 4 * kk);
+#pragma unroll
+                for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        acc[a2][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[kk][a2], bh[kk][b], acc[a2][b], 0, 0, 0);
+                        acc[a2][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk][a2], bl[kk][b], acc[a2][b], 0, 0, 0);
+                        acc[a2][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk][a2], bh[kk][b], acc[a2][b], 0, 0, 0);
+                    }
+            }
+        }
+    } else {
+        for (int ks = 0; ks < nks; ++ks) {
+            const int buf = ks & 1;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's stage-ks DMAs
+            __builtin_amdgcn_s_barrier();                          // every wave's
+            const bool more = ks + 1 < nks;
+#pragma unroll
+            for (int kk = 0; kk < kPK2 / 16; ++kk) {
+                if (more) issue4(ks + 1, buf ^ 1, 4 * kk);
+                bf16x8 ah[2], al[2], bh[4], bl[4];
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    ah[m] = frag(buf, 0, wr * 64 + m * 32 + r, kk);
+                    al[m] = frag(buf, 1, wr * 64 + m * 32 + r, kk);
+                }
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    bh[m] = frag(buf, 2, wc * 128 + m * 32 + r, kk);
+                    bl[m] = frag(buf, 3, wc * 128 + m * 32 + r, kk);
+                }
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+                    }
+            }
         }
     }
-    // epilogue: D2 = |a_i|^2 + |a_j|^2 - 2 <a_i, a_j>; C layout of 32x32: col = lane & 31,
-    // row = (e & 3) + 8 (e >> 2) + 4 h.  Diagonal tiles keep the upper triangle (tj >= ti, the
-    // value gram_pk_kernel stores there) and write it in both orientations.
     if (diag_epi == 1) {   // GLL_GRAM_DIAG = 1 (timing diagnostic): no epilogue, D2 as it was
         float s = 0.f;
 #pragma unroll
@@ -1871,6 +1899,9 @@ __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict_
         if (s == 1234.5f) D2[0] = s;   // keeps the MFMAs alive
         return;
     }
+    // epilogue: D2 = |a_i|^2 + |a_j|^2 - 2 <a_i, a_j>; C layout of 32x32: col = lane & 31,
+    // row = (e & 3) + 8 (e >> 2) + 4 h.  Diagonal tiles keep the upper triangle (tj >= ti, the
+    // value gram_pk_kernel stores there) and write it in both orientations.
     const bool diag = bi == bj;
     if (!diag && diag_epi == 0) {
         // Off-diagonal tiles (round 3): the mirrored orientation leaves the registers as one
@@ -2065,21 +2096,18 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         prof_begin(GLL_K_GRAM, s);
         prof_span(2);
         const dim3 sgrid((L.n + 3) / 4, bt.B);
-        // 40-bit call tag: a random start per process, then one step per call
-        static std::atomic<unsigned long long> gen_ctr{
-            (std::chrono::steady_clock::now().time_since_epoch().count() * 0x9E3779B97F4A7C15ull) ^
-            (unsigned long long)(uintptr_t)&gen_ctr};
-        const unsigned long long gen = (++gen_ctr) & ((1ull << 40) - 1);
-        auto* d2s = L.at<unsigned long long>(ws, L.d2s);
+        float* d2s = L.at<float>(ws, L.d2s);
         if (vec)
-            launch_k(gram_split_kernel<true>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws, d2s, gen);
+            launch_k(gram_split_kernel<true>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
         else
-            launch_k(gram_split_kernel<false>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws, d2s, gen);
+            launch_k(gram_split_kernel<false>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
         const bool H = d2_half(L, bt);
         const int T2 = (L.n + 255) / 256;
         static const int gram_diag = getenv("GLL_GRAM_DIAG") ? atoi(getenv("GLL_GRAM_DIAG")) : 0;
+        static const bool gram_pipe = getenv("GLL_GRAM_PIPE") && atoi(getenv("GLL_GRAM_PIPE")) != 0;
         if (gram_tile256(L, bt, T, T2))
-            launch_k(H ? gram_pk2_kernel<true> : gram_pk2_kernel<false>,
+            launch_k(H ? (gram_pipe ? gram_pk2_kernel<true, true> : gram_pk2_kernel<true, false>)
+                       : (gram_pipe ? gram_pk2_kernel<false, true> : gram_pk2_kernel<false, false>),
                      dim3(unsigned(bt.B * T2 * (T2 + 1) / 2)), 512, 0, s, Ph, Pl, nrm, L.n, L.dp,
                      T2, D2, L.ldD, bt.ws, gram_diag, d2s);
         else
@@ -2151,7 +2179,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     const int planes = gram_planes(L, bt.B);
     dim3 grid((rows + 3) / 4, bt.B);
     const bool h16 = planes == 1 && d2_half(L, bt);   // the Gram stored D2 as fp16 x s
-    const auto* d2s = L.at<unsigned long long>(ws, L.d2s);
+    const float* d2s = L.at<float>(ws, L.d2s);
     prof_begin(GLL_K_SELECT, s);
 // Batched launches (PG = 1) stage x_i in LDS (XQ quarters of 256 features, d <= 1024) and run at
 // 6 waves per SIMD: measured at B = 64 NS, select 259 -> 214 us (XQ = 2, NU = 8; the NU = 16
