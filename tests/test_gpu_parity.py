@@ -854,6 +854,25 @@ def test_fp16_distance_storage_matches_fp32(cfg, B, scale):
     np.testing.assert_array_equal(gh, gf)
 
 
+def test_batched_graphs_stay_independent_with_non_finite_and_large_features():
+    """Per-graph state of a batched launch (workspace block, fp16 D2 scale, CG columns): one
+    graph with a NaN feature row and another scaled by 1e4 leave the other graphs' U and grad_X
+    bitwise what they are in a batch without them, and the call returns (no hang, no fault)."""
+    from graphlearninglayer_amd.synth import seeded_gbar
+    B = 8
+    Xs, Ys, c = _synth_batch("ns", B, seed0=81)
+    G = np.stack([seeded_gbar(c["batch"], 10, 900 + g) for g in range(B)])
+    U0, g0 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G)
+    Xb = Xs.copy()
+    Xb[2, 700, :] = np.nan
+    Xb[5] *= 1e4
+    U1, g1 = _fwd_bwd_batched_c_abi(Xb, Ys, c["k"], 0.07, 1.0, G)
+    for g in (0, 1, 3, 4, 6, 7):
+        np.testing.assert_array_equal(U1[g], U0[g])
+        np.testing.assert_array_equal(g1[g], g0[g])
+    assert np.isfinite(U1[5]).all()
+
+
 @pytest.mark.parametrize("C", [10, 7])
 def test_batched_column_pair_cg_matches_one_column_kernel_bitwise(C):
     """Batched per-column CG on column pairs (solve.hip cg_ell2_kernel, GLL_FLAG_CG_PAIRS; a
