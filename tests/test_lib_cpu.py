@@ -63,6 +63,24 @@ def test_workspace_bytes_and_validation():
     assert lib.gll_strerror(-2).decode().startswith("unsupported")
 
 
+def test_every_launched_kernel_has_device_code():
+    """Every kernel the host code launches (a __device_stub__ in libgll.so) has its kernel
+    descriptor (<name>.kd) in the embedded gfx950 code object: a host pass and a device pass
+    compiled from different versions of a source (an object rebuilt while its file changed)
+    would otherwise fail only at run time ('Cannot find Symbol'), on the GPU."""
+    import re
+    data = open(os.path.join(ROOT, "graphlearninglayer_amd", "libgll.so"), "rb").read()
+    stubs = set(re.findall(rb"_ZN3gll(\d+)__device_stub__([A-Za-z0-9_]+)", data))
+    kds = set(re.findall(rb"(_ZN3gll[0-9]+[A-Za-z0-9_]+)\.kd", data))
+    assert stubs and kds
+    missing = []
+    for ln, rest in stubs:
+        name = b"_ZN3gll" + str(int(ln) - len("__device_stub__")).encode() + rest
+        if name not in kds:
+            missing.append(name.decode())
+    assert missing == [], missing[:5]
+
+
 def test_workspace_row_panels():
     """The distance buffer is n x n up to 32 GiB and a row panel past it (include/gll.h
     GLL_FLAG_KNN_PANEL; gll_internal.h panel_rows): forced panels of 1,024 rows shrink the
