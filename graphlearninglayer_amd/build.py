@@ -49,12 +49,32 @@ def _compile(unit, force, verbose, extra, objdir=OBJ):
     cmd = [hipcc(), *FLAGS, *extra, "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed on {unit}:\n{r.stdout}\n{r.stderr}")
+    for _ in range(3):
+        # hipcc reads the source once per pass (host, device): a file edited mid-compile gives an
+        # object whose host stubs and device code disagree, and a newer mtime than the edit.
+        # Compare the inputs before and after; on a change, compile again.
+        before = _inputs_digest(src)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {unit}:\n{r.stdout}\n{r.stderr}")
+        if _inputs_digest(src) == before:
+            break
+    else:
+        os.remove(obj)
+        raise RuntimeError(f"{unit} kept changing while it compiled")
     if verbose and r.stderr.strip():
         print(r.stderr, file=sys.stderr)
     return obj
+
+
+def _inputs_digest(src):
+    import hashlib
+    h = hashlib.sha256()
+    hs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h"))
+    for f in [src, *hs, os.path.join(INCLUDE, "gll.h")]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
 
 
 TRACE_OBJ = os.path.join(OBJ, "trace")
