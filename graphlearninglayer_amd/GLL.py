@@ -22,7 +22,6 @@ Deliberate differences from the reference (all documented in DESIGN.md):
 """
 from __future__ import annotations
 
-import collections
 import ctypes as ct
 import warnings
 
@@ -33,6 +32,8 @@ from . import _lib
 
 DEFAULT_K = 25          # GLL.py:27
 MAX_K = 57              # include/gll.h: 2 <= K <= 57 (neighbours incl. self; kMaxKm1 = 56)
+DEFAULT_RTOL = 1e-6     # SURVEY.md §8c: fp32 Jacobi-CG at 1e-6 matches SuperLU to <1e-5
+DEFAULT_MAX_ITER = 1000
 
 
 def _check_k(k, n):
@@ -42,38 +43,40 @@ def _check_k(k, n):
     if kk < 2 or kk > MAX_K:
         raise ValueError(f"k = {k} (n = {n}): the kNN count incl. self must satisfy "
                          f"2 <= min(k, n) <= {MAX_K}")
-DEFAULT_RTOL = 1e-6     # SURVEY.md §8c: fp32 Jacobi-CG at 1e-6 matches SuperLU to <1e-5
-DEFAULT_MAX_ITER = 1000
-
-# Device status -> the reference's warnings, without a host sync on the hot path: every
-# call's kernels OR/max/add their status words into a sticky per-device sink (gll_problem.
-# status_sink); every FLUSH_EVERY calls the sink is copied to pinned memory and cleared on
-# the stream, and completed copies are turned into warnings at the next call.
-FLUSH_EVERY = 64
-_pending = collections.deque()
-_sinks = {}
-
-# Optional exploding-gradient diagnostic of the adversarial scripts' inline copy
-# (train_and_adversarial.py:177-183): None = off; a float = the matrix-norm threshold.  When on,
-# calls take the Python Function path, whose backward synchronises to test the norm.
-_grad_diag = None
 
 
-def set_grad_diagnostics(threshold=10.0):
-    """Print the reference's 'possible exploding gradient' report when ||grad_X||_F exceeds
-    `threshold` (the inline copy uses 10); None switches the check off (the default)."""
-    global _grad_diag
-    _grad_diag = None if threshold is None else float(threshold)
+def _load_ext():
+    """_gll_torch.so: LaplaceLearningSparseHard.apply in native code (csrc/torch_ext.cpp) and
+    the per-device status sink.  Built in-tree with libgll.so; there is no fallback."""
+    try:
+        from . import _gll_torch
+    except ImportError as e:
+        raise ImportError("graphlearninglayer_amd: _gll_torch.so is missing or does not load "
+                          "(build it: python -m graphlearninglayer_amd.build). There is no "
+                          f"CPU fallback. ({e})") from e
+    return _gll_torch
 
 
-def _sink(dev: torch.device):
-    s = _sinks.get(dev.index)
-    if s is None:
-        s = _sinks[dev.index] = [torch.zeros(_lib.ST_NWORDS, dtype=torch.int32, device=dev), 0]
-    return s
+_ext_mod = _load_ext()
+
+
+def _ext():
+    return _ext_mod
+
+
+# Device status -> the reference's warnings, without a host sync on the hot path: every call's
+# kernels OR/max/add their status words into a sticky per-device sink (gll_problem.status_sink,
+# owned by _gll_torch); every 64 calls the sink is copied to pinned memory and cleared on the
+# stream, and completed copies are turned into warnings (GLL.py:240-241, 273-274) at a later
+# call, or at check_status().
+def check_status():
+    """Flush every device's status sink now and raise the pending warnings (syncs)."""
+    _ext_mod.check_status()
 
 
 def _warn_from(st):
+    """The warnings / error of one copy of the status words (as _gll_torch raises them), for
+    callers of the C ABI that read the words themselves."""
     if st[_lib.ST_SOLVE_FAILED]:
         raise RuntimeError("GLL: a whole-GPU CG solve lost a grid barrier (a workgroup never "
                            "arrived); its outputs were written as NaN")
@@ -87,41 +90,16 @@ def _warn_from(st):
                       f"max_iter ({st[_lib.ST_BWD_ITERS]} iterations)", RuntimeWarning)
 
 
-def _poll_status(block: bool = False):
-    while _pending:
-        ev, host = _pending[0]
-        if not block and not ev.query():
-            return
-        ev.synchronize()
-        _pending.popleft()
-        _warn_from(host.tolist())
+def _poll_status(dev=None):
+    idx = torch.cuda.current_device() if dev is None else dev.index
+    _ext_mod.poll_status(idx)
 
 
-def _flush(dev: torch.device):
-    s = _sink(dev)
-    host = torch.empty(_lib.ST_NWORDS, dtype=torch.int32, pin_memory=True)
-    host.copy_(s[0], non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record()
-    s[0].zero_()
-    s[1] = 0
-    _pending.append((ev, host))
-
-
-def _after_call(dev: torch.device):
-    s = _sink(dev)
-    s[1] += 1
-    if s[1] >= FLUSH_EVERY:
-        _flush(dev)
-
-
-def check_status():
-    """Flush every device's status sink now and raise the pending warnings (syncs)."""
-    for idx in list(_sinks):
-        dev = torch.device("cuda", idx)
-        with torch.cuda.device(dev):
-            _flush(dev)
-    _poll_status(block=True)
+def set_grad_diagnostics(threshold=10.0):
+    """Print the reference's 'possible exploding gradient' report when ||grad_X||_F exceeds
+    `threshold` (the inline copy of train_and_adversarial.py:177-183 uses 10) for calls made
+    from now on; None switches the check off (the default).  The check synchronises."""
+    _ext_mod.set_grad_diagnostics(-1.0 if threshold is None else float(threshold))
 
 
 def _device_for(X: torch.Tensor) -> torch.device:
@@ -176,58 +154,28 @@ def _stream(dev) -> int:
     return torch.cuda.current_stream(dev).cuda_stream
 
 
-_ext_mod = None
-
-
-def _ext():
-    """The C++ autograd node (_gll_torch.so, built with libgll.so); None if not built."""
-    global _ext_mod
-    if _ext_mod is None:
-        try:
-            from . import _gll_torch
-            _ext_mod = _gll_torch
-        except ImportError:
-            _ext_mod = False
-    return _ext_mod or None
-
-
 class LaplaceLearningSparseHard(torch.autograd.Function):
     """Graph Laplace learning layer; labeled rows of X come first (GLL.py:11).
 
-    `LaplaceLearningSparseHard.apply(X, label_matrix, tau=0, epsilon='auto'[, k=25])` runs
-    the C++ autograd node of _gll_torch.so (host overhead ~20 us instead of ~150 us for a
-    Python Function); when that module was not built, the Python Function below (ctypes
-    onto the same C ABI) is used.  Both execute only the HIP kernels of libgll.so."""
+    `LaplaceLearningSparseHard.apply(X, label_matrix, tau=0, epsilon='auto'[, k=25])` is the
+    native function of _gll_torch.so (csrc/torch_ext.cpp): argument checks, the forward
+    kernels and one autograd node whose backward runs the backward kernels -- the whole host
+    side of a call in C++.  `apply_python` is the same call as a Python
+    torch.autograd.Function over the ctypes binding of the same C ABI (tests compare the two
+    bitwise).  Both execute only the HIP kernels of libgll.so."""
 
-    @classmethod
-    def apply(cls, X, label_matrix, tau=0, epsilon="auto", k=DEFAULT_K):
-        _check_k(k, X.shape[-2])
-        ext = _ext()
-        if ext is None or _grad_diag is not None:
-            return super().apply(X, label_matrix, tau, epsilon, k)
-        if _pending:
-            _poll_status()
-        dev = X.device if X.is_cuda else _device_for(X)
-        s = _sinks.get(dev.index)
-        if s is None:
-            s = _sink(dev)
-        U = ext.laplace_learning(X, label_matrix, float(tau), _eps_value(epsilon), int(k),
-                                 DEFAULT_MAX_ITER, DEFAULT_RTOL, s[0].data_ptr())
-        s[1] += 1
-        if s[1] >= FLUSH_EVERY:
-            with torch.cuda.device(dev):
-                _flush(dev)
-        return U
+    apply = staticmethod(_ext_mod.apply)
 
     @classmethod
     def apply_python(cls, X, label_matrix, tau=0, epsilon="auto", k=DEFAULT_K):
         """The Python torch.autograd.Function path (ctypes onto the same C ABI)."""
+        _check_k(k, X.shape[-2])
         return super().apply(X, label_matrix, tau, epsilon, k)
 
     @staticmethod
     def forward(ctx, X, label_matrix, tau=0, epsilon="auto", k=DEFAULT_K):
-        _poll_status()
         dev = _device_for(X)
+        _poll_status(dev)
         if X.dim() not in (2, 3) or label_matrix.dim() not in (2, X.dim()):
             raise ValueError("X must be n x d (or B x n x d), label_matrix base x C "
                              "(or B x base x C)")
@@ -242,7 +190,7 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
             if X.dim() == 3 and Y.shape[0] != B:
                 raise ValueError(f"label_matrix batch {Y.shape[0]} != {B}")
             prob = make_problem(n, d, base, C, k, tau, epsilon)
-            prob.status_sink = _sink(dev)[0].data_ptr()
+            prob.status_sink = _ext_mod.status_sink(dev.index)
             nbytes = _lib.lib().gll_workspace_bytes(ct.byref(prob))
             if nbytes == 0:
                 raise ValueError(f"unsupported GLL problem n={n} d={d} base={base} C={C} k={k}")
@@ -252,7 +200,7 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
                                                       Y.data_ptr(), ydt, ws.data_ptr(),
                                                       U.data_ptr(), _stream(dev)),
                        "gll_forward")
-            _after_call(dev)
+            _ext_mod.note_call(dev.index)
         ctx.save_for_backward(X)
         ctx.prob, ctx.ws, ctx.dev, ctx.B = prob, ws, dev, B
         return U if X.is_cuda else U.cpu()
@@ -271,20 +219,6 @@ class LaplaceLearningSparseHard(torch.autograd.Function):
                                                        ctx.ws.data_ptr(), g.data_ptr(), gdt,
                                                        gradX.data_ptr(), _stream(dev)),
                        "gll_backward")
-        if _grad_diag is not None:
-            out_norm = torch.linalg.vector_norm(gradX).item()
-            if out_norm > _grad_diag:     # train_and_adversarial.py:177-183
-                m = prob.n - prob.base
-                wadj = ctx.ws.new_empty(0)
-                view = _lib.View()
-                _lib.check(_lib.lib().gll_workspace_view(ct.byref(prob), ctx.ws.data_ptr(),
-                                                         ct.byref(view)), "gll_workspace_view")
-                off = view.wadj - ctx.ws.data_ptr()
-                wadj = ctx.ws[off: off + 4 * m * prob.C].view(torch.float32)
-                print("possible exploding gradient")
-                print("grad norm: ", torch.linalg.vector_norm(g.double()).item())
-                print("w norm: ", torch.linalg.vector_norm(wadj.double()).item())
-                print("out norm: ", out_norm)
         if gradX.device != X.device or gradX.dtype != X.dtype:
             gradX = gradX.to(device=X.device, dtype=X.dtype)
         return gradX, None, None, None, None

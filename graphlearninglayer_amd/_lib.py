@@ -14,24 +14,21 @@ LIB_PATH = os.environ.get("GLL_LIB_PATH") or os.path.join(HERE, "libgll.so")  # 
 
 GLL_OK = 0
 GLL_DT_F32, GLL_DT_F64, GLL_DT_I64 = 0, 1, 2
-FLAG_CG_GRID = 1   # gll_problem.flags: force the whole-GPU CG (include/gll.h)
-FLAG_GRAM_NARROW = 2   # gll_problem.flags: 64-tile Gram everywhere (diagnostic)
-FLAG_CG_CLASSIC = 4   # gll_problem.flags: two-reduction per-column PCG (diagnostic)
-FLAG_CG_PERCOL = 8   # gll_problem.flags: per-column CG for large single graphs (diagnostic)
-FLAG_GRAM_F32 = 16   # gll_problem.flags: retired (fp32-MFMA Gram kernels removed); rejected
-FLAG_CG_PIPE = 32    # gll_problem.flags: pipelined per-column PCG (diagnostic)
-FLAG_GRAM_NOSPLIT = 64   # gll_problem.flags: unsplit Gram tiles for small single graphs (diagnostic)
+# gll_problem.flags (include/gll.h): code-path choices for tests and A/B runs
+FLAG_CG_GRID = 1          # force the whole-GPU CG
+FLAG_CG_PERCOL = 8        # per-column CG for large single graphs
 FLAG_DIAG_GRID_OVERSUB = 128   # tests: whole-GPU CG grid past co-residency (launch refused)
-FLAG_DIAG_GRID_FAIL = 256      # tests: injected grid-barrier failure (NaN + ST_SOLVE_FAILED)
-FLAG_CG_ELL = 512   # gll_problem.flags: register-ELL per-column CG where the balanced one runs
-FLAG_CG_VR = 1024   # gll_problem.flags: balanced (virtual-row) per-column CG wherever it fits
-FLAG_GRAD_ROWS = 2048   # gll_problem.flags: whole-row feature-gradient kernel (diagnostic)
-FLAG_GRAD_CHUNK = 4096  # gll_problem.flags: feature-chunked gradient kernel wherever it runs
-FLAG_GRAM_INLINE = 8192  # gll_problem.flags: 128-tile Gram with the inline split (diagnostic)
-FLAG_BWD_UNFUSED = 16384  # gll_problem.flags: adjoint CG and gradient as two launches (diagnostic)
-FLAG_CG_PAIRS = 32768   # gll_problem.flags: batched per-column CG on column pairs (diagnostic)
-FLAG_KNN_PANEL = 65536   # gll_problem.flags: kNN in row panels (O(panel x n) distances)
-FLAG_D2_F32 = 131072   # gll_problem.flags: fp32 distance matrix on the pre-split Gram route (diagnostic)
+FLAG_DIAG_GRID_FAIL = 256      # tests: injected grid-barrier failure
+FLAG_CG_ELL = 512         # register-ELL per-column CG where the balanced one runs
+FLAG_CG_VR = 1024         # balanced (virtual-row) per-column CG wherever it fits
+FLAG_GRAD_ROWS = 2048     # whole-row feature-gradient kernel
+FLAG_GRAD_CHUNK = 4096    # feature-chunked gradient kernel wherever it runs
+FLAG_GRAM_INLINE = 8192   # 128-tile Gram with the inline split
+FLAG_BWD_UNFUSED = 16384  # adjoint CG and gradient as two launches
+FLAG_KNN_PANEL = 65536    # kNN in row panels (O(panel x n) distances)
+FLAG_D2_F32 = 131072      # fp32 distance matrix on the pre-split Gram route
+# process-wide test knobs (gll_set_knob): force a code path, 0 = automatic
+KNOB_VR_RV, KNOB_GRID_CAP, KNOB_GRAM_TILE = 0, 1, 2
 ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
 ST_KNN_RESCAN = 5   # kNN rows re-ranked over every column under the Gram error bound
 ST_SOLVE_FAILED = 6   # a whole-GPU CG lost a grid barrier: outputs NaN, raised as an error
@@ -45,7 +42,7 @@ EXPORTS = (
     "gll_workspace_bytes", "gll_forward", "gll_backward", "gll_forward_batched",
     "gll_backward_batched", "gll_graph", "gll_workspace_view",
     "gll_cg_csr_workspace_bytes", "gll_cg_csr", "gll_prof_enable", "gll_prof_read",
-    "gll_kernel_name", "gll_strerror",
+    "gll_kernel_name", "gll_strerror", "gll_set_knob",
 )
 
 
@@ -94,6 +91,8 @@ def _declare(lib):
     lib.gll_prof_read.restype = i32
     lib.gll_kernel_name.argtypes = [i32]
     lib.gll_kernel_name.restype = ct.c_char_p
+    lib.gll_set_knob.argtypes = [i32, i32]
+    lib.gll_set_knob.restype = i32
     lib.gll_strerror.argtypes = [i32]
     lib.gll_strerror.restype = ct.c_char_p
     return lib
@@ -131,3 +130,8 @@ def prof_read(kid: int):
     ms, cnt = ct.c_double(0.0), ct.c_int(0)
     check(lib().gll_prof_read(kid, ct.byref(ms), ct.byref(cnt)), "gll_prof_read")
     return ms.value, cnt.value
+
+
+def set_knob(knob: int, value: int):
+    """Force a code path for tests (include/gll.h GLL_KNOB_*); 0 restores the automatic one."""
+    check(lib().gll_set_knob(int(knob), int(value)), "gll_set_knob")

@@ -4,9 +4,11 @@
 // stream.  No allocation, no host synchronisation: the caller owns the workspace (the
 // Python mirror takes it from torch's caching allocator) and keeps it alive from
 // gll_forward to gll_backward, as the reference keeps its graph on ctx (GLL.py:69-70).
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "gll_internal.h"
@@ -70,11 +72,82 @@ void prof_end(int kid, hipStream_t) {
     g_armed = ArmedLaunch{};
 }
 
+bool debug_log() {
+    static const bool dbg = getenv("GLL_DEBUG") != nullptr;
+    return dbg;
+}
+
 hipError_t launch_status(const char* what) {
     const hipError_t e = hipGetLastError();
-    static const bool dbg = getenv("GLL_DEBUG") != nullptr;
-    if (e != hipSuccess && dbg) fprintf(stderr, "gll: %s: %s\n", what, hipGetErrorString(e));
+    if (e != hipSuccess && debug_log()) fprintf(stderr, "gll: %s: %s\n", what, hipGetErrorString(e));
     return e;
+}
+
+// ---------------------------------------------------------------------------------------
+// Test knobs and cached device facts (gll_internal.h)
+// ---------------------------------------------------------------------------------------
+static std::atomic<int> g_knobs[GLL_KNOB_COUNT];
+
+int knob(int id) { return g_knobs[id].load(std::memory_order_relaxed); }
+
+static constexpr int kMaxDev = 64;
+static std::atomic<int> g_cus[kMaxDev];
+
+int device_cus() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= kMaxDev) dev = 0;
+    int v = g_cus[dev].load(std::memory_order_relaxed);
+    if (v <= 0) {
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            v = 0;
+        (void)hipGetLastError();
+        v = v > 0 ? v : 1;
+        g_cus[dev].store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
+
+namespace {
+struct OccKey {
+    const void* fn;
+    int nt;
+    size_t lds;
+    bool operator==(const OccKey& o) const { return fn == o.fn && nt == o.nt && lds == o.lds; }
+};
+struct OccHash {
+    size_t operator()(const OccKey& k) const {
+        return std::hash<const void*>()(k.fn) ^ (size_t(k.nt) << 20) ^ (k.lds * 0x9E3779B97F4A7C15ull);
+    }
+};
+std::mutex g_occ_mu;
+std::unordered_map<OccKey, int, OccHash> g_occ;
+std::unordered_map<const void*, size_t> g_slds;
+}  // namespace
+
+// (one device model per process: MI355X nodes are homogeneous)
+int occupancy_blocks(const void* fn, int nt, size_t lds) {
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    const OccKey key{fn, nt, lds};
+    auto it = g_occ.find(key);
+    if (it != g_occ.end()) return it->second;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, nt, lds) != hipSuccess) nb = 0;
+    (void)hipGetLastError();
+    g_occ.emplace(key, nb);
+    return nb;
+}
+
+size_t static_lds_bytes(const void* fn) {
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    auto it = g_slds.find(fn);
+    if (it != g_slds.end()) return it->second;
+    hipFuncAttributes at{};
+    size_t stat = 8192;
+    if (hipFuncGetAttributes(&at, fn) == hipSuccess) stat = at.sharedSizeBytes;
+    (void)hipGetLastError();
+    g_slds.emplace(fn, stat);
+    return stat;
 }
 
 static const char* kKernelNames[GLL_K_COUNT] = {
@@ -91,7 +164,7 @@ static int check(const gll_problem* p) {
     if (p->base < 0 || p->base > p->n) return GLL_ERR_INVALID_ARG;
     const int K = p->K < p->n ? p->K : p->n;
     if (K - 1 > kMaxKm1) return GLL_ERR_UNSUPPORTED;  // candidate lists + rescan lanes
-    if (p->flags & GLL_FLAG_GRAM_F32) return GLL_ERR_UNSUPPORTED;   // retired (round 2)
+    if (p->flags & ~GLL_FLAG_ALL) return GLL_ERR_INVALID_ARG;   // unknown (or retired) flags
     if (p->C > 256) return GLL_ERR_UNSUPPORTED;       // rhs accumulators per lane
     if ((p->d + 255) / 256 > 16) return GLL_ERR_UNSUPPORTED;  // d <= 4096 in the SpMM
     if (int64_t(p->n) * K > INT32_MAX / 2) return GLL_ERR_UNSUPPORTED;
@@ -290,6 +363,12 @@ int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const f
 size_t gll_cg_csr_workspace_bytes(int m, int C) {
     const size_t per_col = size_t(5) * m * C, grid = grid_cg_workspace_floats(m, C);
     return (per_col > grid ? per_col : grid) * sizeof(float);
+}
+
+int gll_set_knob(int id, int value) {
+    if (id < 0 || id >= GLL_KNOB_COUNT || value < 0) return GLL_ERR_INVALID_ARG;
+    g_knobs[id].store(value, std::memory_order_relaxed);
+    return GLL_OK;
 }
 
 int gll_prof_enable(int kid, int period) {

@@ -47,17 +47,26 @@ constexpr int kVrSlot = kVS * 2 + kVS * 4;   // 48 B
 // hold at most 5 in 128 VGPRs and spilled: 118 against 66 us per FullySup solve)
 constexpr int kVrNT = 512;
 inline int vr_max_per_row(int K) { return ((K - 1) + 4 * (K - 1) + 8 + kVS - 1) / kVS; }
+
+// Process-wide test knobs (gll_set_knob, include/gll.h): each forces a code path, never a result.
+// An atomic load, not a getenv per call (host time on the step's critical path).
+int knob(int id);
+// Set GLL_DEBUG=1 in the environment to print launch failures (read once).
+bool debug_log();
+// Device facts the launchers need, queried once per device / kernel and cached for the process.
+int device_cus();                                          // CUs of the current device
+int occupancy_blocks(const void* fn, int nt, size_t lds);  // resident blocks per CU
+size_t static_lds_bytes(const void* fn);                   // the kernel's static LDS
+
 inline int vr_threads(int n, int m, int K, int flags) {
     if (m <= 0 || m > 4 * kVrNT || (flags & GLL_FLAG_CG_ELL)) return 0;
-    if (flags & (GLL_FLAG_CG_CLASSIC | GLL_FLAG_CG_PIPE)) return 0;
     // kNN union rows hold ~1.4 (K-1) entries, a fraction m/n of them in the U block
     const double len = 1.4 * (K - 1) * double(m) / double(n);
     if (len <= 12.0 && !(flags & GLL_FLAG_CG_VR)) return 0;
     const double v = m * (len / kVS + 0.5);
     int rv = int((v + kVrNT - 1) / kVrNT);
     // tests: force the register capacity (4 at K = 25 puts most rows on the CSR spill path)
-    const char* force = getenv("GLL_VR_RV");
-    if (force) rv = atoi(force);
+    if (knob(GLL_KNOB_VR_RV) > 0) rv = knob(GLL_KNOB_VR_RV);
     return rv <= 4 ? 4 : (rv <= 8 ? 8 : (rv <= 10 ? 10 : 0));
 }
 
@@ -139,15 +148,13 @@ inline int gram_splits(int n, int d) {
 
 // Rows of the squared-distance buffer: n (the whole n x n matrix), or a panel of PR rows when
 // the matrix would pass 32 GiB (panels of 8 GiB) or GLL_FLAG_KNN_PANEL asks for panels of 1,024
-// rows (GLL_PANEL_ROWS overrides both; diagnostic).  The kNN is then built panel by panel:
-// rectangular Gram tiles of the panel's rows against every column, then the select of those
-// rows (api.hip build_graph).  A multiple of 128 (the Gram tile), < n in panel mode.
+// rows.  The kNN is then built panel by panel: rectangular Gram tiles of the panel's rows
+// against every column, then the select of those rows (api.hip build_graph).  A multiple of 128
+// (the Gram tile), < n in panel mode.
 inline int panel_rows(int n, int flags) {
     const size_t row_bytes = size_t((n + 3) & ~3) * 4;
-    static const int env = getenv("GLL_PANEL_ROWS") ? atoi(getenv("GLL_PANEL_ROWS")) : 0;
     int64_t pr = n;
-    if (env > 0) pr = env;
-    else if (flags & GLL_FLAG_KNN_PANEL) pr = 1024;
+    if (flags & GLL_FLAG_KNN_PANEL) pr = 1024;
     else if (size_t(n) * row_bytes > (size_t(32) << 30)) pr = int64_t((size_t(8) << 30) / row_bytes);
     if (pr >= n) return n;
     pr = (pr / 128) * 128;
@@ -177,7 +184,8 @@ struct Layout {
     size_t vr;        // [m][VRM] packed virtual rows (kVrSlot bytes each)
     int dp;           // split-Gram planes: d rounded up to 64
     size_t xhi, xlo, xnrm;   // [n][dp] bf16 hi / lo planes of x - x_0, and |x - x_0|^2
-    size_t fsync;     // fused backward: [0] solved columns, [32] finished gradient blocks
+    size_t fsync;     // fused backward: [0] solved columns, [32] finished gradient blocks,
+                      // [64] poison (a lost solve: the counters may be stale)
     size_t d2s;       // float: the fp16 D2 scale of the pre-split GEMM (knn.hip tile_d2_scale)
 
     explicit Layout(const gll_problem& p) {
@@ -227,7 +235,7 @@ struct Layout {
         xhi = take(size_t(n) * dp * 2);
         xlo = take(size_t(n) * dp * 2);
         xnrm = take(size_t(n) * 4);
-        fsync = take(256);   // two counters on their own 128-B lines, zeroed by row_build
+        fsync = take(384);   // three words on their own 128-B lines, zeroed by row_build
         d2s = take(256);     // fp16 D2 scale of the pre-split Gram (knn.hip tile_d2_scale)
         P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)
         Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
@@ -252,10 +260,7 @@ inline int ell_emit(const Layout& L, int B) {
 }
 
 // Planes the Gram kernel of a launch over B graphs writes (= planes the select kernel sums).
-inline int gram_planes(const Layout& L, int B) {
-    if (L.flags & GLL_FLAG_GRAM_NOSPLIT) return 1;
-    return (L.KS == 2 && B == 1) ? 2 : 1;
-}
+inline int gram_planes(const Layout& L, int B) { return (L.KS == 2 && B == 1) ? 2 : 1; }
 
 // ---------------------------------------------------------------------------------------
 // Device helpers

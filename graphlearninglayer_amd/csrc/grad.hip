@@ -331,11 +331,9 @@ hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, cons
         e = vec ? grad_nd<true, true, 0>(a, bt, X, gradX, s)
                 : grad_nd<true, false, 0>(a, bt, X, gradX, s);
     } else {
-        // fixed eps: inline coefficient in register form (diagnostic GLL_GRAD_CV=0 keeps the
-        // generic loop, for A/B)
-        static const bool generic = getenv("GLL_GRAD_CV") && atoi(getenv("GLL_GRAD_CV")) == 0;
-        // (ten classes: every caller's label matrix, FullySup.py:153; other C the generic loop)
-        if (!generic && L.C == 10)
+        // fixed eps: inline coefficient in register form for ten classes (every caller's label
+        // matrix, FullySup.py:153; other C the generic loop)
+        if (L.C == 10)
             e = vec ? grad_nd<false, true, -10>(a, bt, X, gradX, s)
                     : grad_nd<false, false, -10>(a, bt, X, gradX, s);
         else

@@ -905,79 +905,29 @@ size_t grid_cg_workspace_floats(int m, int C) {
     return classic > gv ? classic : gv;
 }
 
-static int cu_count() {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, v = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
-        cus = v > 0 ? v : 1;
-    }
-    return cus;
-}
-
 // Workgroups of one kernel instance that can be resident at once on the whole device (the
 // classic kernel, no dynamic LDS).
 template <class Mat, int LPR, int RPG>
 static int coresident_capacity() {
     static int cap = -1;
     if (cap < 0) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void*>(cg_grid_classic_kernel<Mat, LPR, RPG>), kGT, 0) !=
-            hipSuccess)
-            nb = 1;
-        (void)hipGetLastError();
-        cap = (nb > 0 ? nb : 1) * cu_count();
+        const int nb = occupancy_blocks(
+            reinterpret_cast<const void*>(cg_grid_classic_kernel<Mat, LPR, RPG>), kGT, 0);
+        cap = (nb > 0 ? nb : 1) * device_cus();
     }
     return cap;
 }
 
-// GLL_GRID_COOP=1: start the grid with hipLaunchCooperativeKernel (diagnostic).  The default
-// is an ordinary launch sized within the co-resident capacity: MI355X_MICROARCH.md's price
-// list puts the cooperative launch at +15-19 us of host time per launch for no residency the
-// ordinary launch lacks (the runtime's check even accepts one workgroup per CU more than the
-// hardware admits at some SGPR counts), and under rocprofv3 a process that made one crashed
-// at exit.  The bounded barrier turns any residency failure into NaN outputs
-// + GLL_ST_SOLVE_FAILED instead of a hang.
-static bool coop_requested() {
-    static int v = -1;
-    if (v < 0) {
-        int dev = 0, a = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&a, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess) a = 0;
-        (void)hipGetLastError();
-        const char* env = getenv("GLL_GRID_COOP");
-        v = (a != 0 && env && env[0] == '1') ? 1 : 0;
-    }
-    return v == 1;
-}
-
-static int env_int(const char* name, int dflt) {   // read per call (tests set them)
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-
+// An ordinary launch sized within the co-resident capacity.  MI355X_MICROARCH.md's price list
+// puts hipLaunchCooperativeKernel at +15-19 us of host time per launch for no residency the
+// ordinary launch lacks (its check even accepts one workgroup per CU more than the hardware
+// admits at some SGPR counts), and under rocprofv3 a process that made one crashed at exit
+// (DESIGN.md §3.2); the cooperative variant was removed in round 4.  The bounded barrier turns
+// a residency failure into GLL_ST_SOLVE_FAILED instead of a hang.
 template <typename F, typename... Args>
 static hipError_t launch_persistent(F fn, int G, int nt, size_t lds, hipStream_t s,
                                     const char* what, Args... args) {
-    if (!coop_requested()) {
-        launch_k(fn, dim3(unsigned(G)), dim3(unsigned(nt)), lds, s, args...);
-        return launch_status(what);
-    }
-    void* argv[] = {&args...};
-    const ArmedLaunch armed = g_armed;   // bench timing: events around the launch
-    g_armed = ArmedLaunch{};
-    if (armed.kid >= 0) (void)hipEventRecord(armed.e0, s);
-    hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(unsigned(G)),
-                                              dim3(unsigned(nt)), argv, unsigned(lds), s);
-    if (armed.kid >= 0) (void)hipEventRecord(armed.e1, s);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        if (getenv("GLL_DEBUG"))
-            fprintf(stderr, "gll: %s (cooperative, G=%d): %s\n", what, G, hipGetErrorString(e));
-        return e;
-    }
+    launch_k(fn, dim3(unsigned(G)), dim3(unsigned(nt)), lds, s, args...);
     return launch_status(what);
 }
 
@@ -1013,7 +963,7 @@ static hipError_t dispatch_classic(const Mat& A, const GridCgArgs& a, int64_t nn
                                  : std::min(coresident_capacity<Mat, 8, 1>(),
                                             coresident_capacity<Mat, 8, 8>());
     cap = std::min<int64_t>(cap, 1024);
-    cap = std::min<int64_t>(cap, std::max(1, env_int("GLL_GRID_CAP", int(cap))));
+    if (knob(GLL_KNOB_GRID_CAP) > 0) cap = std::min<int64_t>(cap, knob(GLL_KNOB_GRID_CAP));
     int rpg = 0;
     int64_t G = 0;
     for (int64_t lim : {std::min<int64_t>(64, cap), cap}) {
@@ -1050,38 +1000,29 @@ static hipError_t launch_gv(const Mat& A, GvArgs a, int G, int64_t nnz, float* w
     allow_full_lds(reinterpret_cast<const void*>(fn));
     // the slice: the workgroup's share of the entries with a quarter of margin (rows beyond it
     // read the CSR), within what the static LDS leaves; unknown nnz (< 0): all of it
-    hipFuncAttributes at{};
-    size_t stat = 8192;
-    if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(fn)) == hipSuccess)
-        stat = at.sharedSizeBytes;
-    (void)hipGetLastError();
+    const size_t stat = static_lds_bytes(reinterpret_cast<const void*>(fn));
     const size_t lds_max = (size_t(160) * 1024 - stat - 256) & ~size_t(15);
     size_t lds = lds_max;
     if (nnz >= 0) {
         const int64_t per = (nnz + G - 1) / G;
         lds = std::min(lds_max, size_t(per + per / 4 + 64) * 8);
     }
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(fn), NT,
-                                                     lds) != hipSuccess)
-        nb = 0;
-    (void)hipGetLastError();
-    if (nb < 1 || G > kMaxG || G > cu_count()) return hipErrorCooperativeLaunchTooLarge;
+    const int nb = occupancy_blocks(reinterpret_cast<const void*>(fn), NT, lds);
+    if (nb < 1 || G > kMaxG || G > device_cus()) return hipErrorCooperativeLaunchTooLarge;
     a.sync = reinterpret_cast<unsigned*>(ws);
     a.V = ws + kSyncWords;                       // 1280 B in: 256-B aligned
     a.part = a.V + size_t(2) * a.m * a.Cp;
     a.lds_cap = int(lds / 8);
     hipError_t e = hipMemsetAsync(a.sync, 0, kSyncWords * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    static const bool dbg = getenv("GLL_DEBUG") != nullptr;
-    if (dbg)
+    if (debug_log())
         fprintf(stderr, "gll: grid CG (%s) G=%d rows/wg=%d NT=%d LPR=%d RPG=%d lds=%zu hier=%d\n",
                 MODE == 0 ? "pipelined" : "Chronopoulos-Gear", G, a.rows_per_wg, NT, LPR, RPG, lds,
                 a.hier);
     return launch_persistent(fn, G, NT, lds, s, "gridcg.hip:launch_gv", A, a);
 }
 
-// Workgroups: one per CU at most, about 16 rows each (GLL_GRID_G overrides, diagnostic);
+// Workgroups: one per CU at most, about 16 rows each;
 // lanes per row as wide as the rows per workgroup allow; up to 512 rows per workgroup (m <=
 // 131,072 at 256 workgroups).  hipErrorNotSupported: no configuration holds it.
 template <class Mat, int MODE>
@@ -1104,17 +1045,15 @@ static hipError_t dispatch_gv(const Mat& A, const GridCgArgs& c, int64_t nnz, fl
     a.st_iters = c.st_iters;
     a.st_nonconv = c.st_nonconv;
     a.st_failed = c.st_failed;
-    a.hier = env_int("GLL_GRID_HIER", 1) != 0 ? 1 : 0;
-    int cap = std::min(kMaxG, cu_count());
-    cap = std::min(cap, std::max(1, env_int("GLL_GRID_CAP", cap)));
+    a.hier = 1;   // XCD-class hierarchical arrivals (a flat counter measured 116 against 74 us)
+    int cap = std::min(kMaxG, device_cus());
+    if (knob(GLL_KNOB_GRID_CAP) > 0) cap = std::min(cap, knob(GLL_KNOB_GRID_CAP));
     int G = int(std::min<int64_t>(cap, (int64_t(a.m) + 15) / 16));
-    const int Gf = env_int("GLL_GRID_G", 0);
-    if (Gf > 0) G = std::min(cap, Gf);
     if (G < 1) G = 1;
     const int R = (a.m + G - 1) / G;
     // 256 threads while lanes per row can stay >= 4 with one row per lane group; 1024 threads
-    // (16 waves: more gathers in flight per CU) for long row blocks (GLL_GRID_NT overrides)
-    const int nt = env_int("GLL_GRID_NT", R <= 64 ? 256 : 1024);
+    // (16 waves: more gathers in flight per CU) for long row blocks
+    const int nt = R <= 64 ? 256 : 1024;
     if (nt == 256) {
         if (R <= 16) return launch_gv<Mat, 256, 16, 1, MODE>(A, a, G, nnz, ws, s);
         if (R <= 32) return launch_gv<Mat, 256, 8, 1, MODE>(A, a, G, nnz, ws, s);
@@ -1130,17 +1069,17 @@ static hipError_t dispatch_gv(const Mat& A, const GridCgArgs& c, int64_t nnz, fl
     return hipErrorNotSupported;
 }
 
-// The pipelined kernel unless GLL_GRID_CLASSIC=1 (A/B) or the oversubscription test asks for
-// the classic sizing; past the pipelined kernel's row capacity, the classic kernel.
+// The pipelined kernel unless the oversubscription test asks for the classic sizing; past the
+// pipelined kernel's row capacity, the classic kernel.
 template <class Mat>
 static hipError_t dispatch_grid(const Mat& A, const GridCgArgs& a, int64_t nnz, float* ws,
                                 bool oversub, hipStream_t s) {
-    if (!oversub && env_int("GLL_GRID_CLASSIC", 0) == 0) {
+    if (!oversub) {
         // Luu solves (rtol 1e-6 relative): pipelined; general CSR (utils.laplace's refinement
-        // sweeps on ill-conditioned systems): Chronopoulos-Gear.  GLL_GRID_MODE overrides.
-        const int mode = env_int("GLL_GRID_MODE", Mat::kSeparateDiag ? 0 : 1);
-        const hipError_t e = mode == 0 ? dispatch_gv<Mat, 0>(A, a, nnz, ws, s)
-                                       : dispatch_gv<Mat, 1>(A, a, nnz, ws, s);
+        // sweeps on ill-conditioned systems): Chronopoulos-Gear
+        hipError_t e;
+        if constexpr (Mat::kSeparateDiag) e = dispatch_gv<Mat, 0>(A, a, nnz, ws, s);
+        else e = dispatch_gv<Mat, 1>(A, a, nnz, ws, s);
         if (e != hipErrorNotSupported) return e;
     }
     return dispatch_classic(A, a, nnz < 0 ? int64_t(a.m) * 8 : nnz, ws, oversub, s);

@@ -1493,7 +1493,7 @@ void knn_select_kernel(
     float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ rev_cnt,
     int32_t* __restrict__ rev_idx, float* __restrict__ rev_d2, int32_t* __restrict__ ovf,
     int32_t* __restrict__ status, int32_t* __restrict__ status_pub, size_t xs, size_t wss,
-    size_t sts, int diag, int r0, int r1, const float* __restrict__ d2s) {
+    size_t sts, int r0, int r1, const float* __restrict__ d2s) {
     GLL_TRACE_SCOPE(1);
     GLL_TRACE_PT(20);
     const int2 gxy = batch_xy<R>();   // once (per pointer it re-reads gridDim and divides)
@@ -1577,14 +1577,6 @@ void knn_select_kernel(
             kce = kc;
         }
     }
-    if (diag == 1) {   // phase timing (GLL_SEL_DIAG, diagnostic): candidates only; the row
-        if (lane < K) {  // keeps self loops only (valid indices, no edges downstream)
-            knn_idx[size_t(i) * K + lane] = ci >= -1 ? i : 0;
-            knn_d2[size_t(i) * K + lane] = 0.f;
-        }
-        if (lane == 0) eps[i] = 1.f;
-        return;
-    }
     // 2b) drop the candidates the Gram's error bound already rules out, before their exact
     //     distances are computed (each is a d-float row gather): with G = the (K-1)-th smallest
     //     Gram D2 among the candidates and B its error bound (kGramErr, below), the exact
@@ -1631,14 +1623,6 @@ void knn_select_kernel(
     double ce = double(exact_d2<VEC, PG, float, NU, XL>(X, xi, i, d, ci, 0, kce,
                                                         __builtin_inff(), &s_xi[wv][0]));
     GLL_TRACE_PT(18);
-    if (diag == 2) {   // phase timing: candidates, prune and exact distances (as diag 1)
-        if (lane < K) {
-            knn_idx[size_t(i) * K + lane] = ce >= -1.0 ? i : 0;
-            knn_d2[size_t(i) * K + lane] = 0.f;
-        }
-        if (lane == 0) eps[i] = 1.f;
-        return;
-    }
     if (ci < 0) ce = __builtin_inf();
     // 4) rank the candidates by (exact d^2, index); keep the K-1 nearest
     int rank = key_rank(ce, ci, kce);
@@ -1755,12 +1739,12 @@ void knn_select_kernel(
 // --------------------------------------------------------------------------------------
 constexpr int kPK2 = 32;   // features per k-stage of the 256-tile kernel
 
-template <bool H, bool PIPE>
+template <bool H>
 __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict__ Ph,
                                                        const __bf16* __restrict__ Pl,
                                                        const float* __restrict__ nrm, int n,
                                                        int dp, int T, float* __restrict__ D2,
-                                                       int ld, size_t wss, int diag_epi,
+                                                       int ld, size_t wss,
                                                        float* __restrict__ d2s) {
     const int NT = T * (T + 1) / 2;
     const int idx = xcd_tile(blockIdx.x, gridDim.x);
@@ -1824,42 +1808,10 @@ __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict_
         dsc = tile_d2_scale<512>(nrm, n, red);
         if (threadIdx.x == 0) *d2s = dsc;
     }
-    if constexpr (PIPE) {
-        // both k-steps' fragments of a stage requested at once (two register sets), so the
-        // second set's LDS reads run under the first set's 24 MFMAs (GLL_GRAM_PIPE, A/B)
-        for (int ks = 0; ks < nks; ++ks) {
-            const int buf = ks & 1;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            const bool more = ks + 1 < nks;
-            bf16x8 ah[2][2], al[2][2], bh[2][4], bl[2][4];
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    ah[kk][m] = frag(buf, 0, wr * 64 + m * 32 + r, kk);
-                    al[kk][m] = frag(buf, 1, wr * 64 + m * 32 + r, kk);
-                }
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    bh[kk][m] = frag(buf, 2, wc * 128 + m * 32 + r, kk);
-                    bl[kk][m] = frag(buf, 3, wc * 128 + m * 32 + r, kk);
-                }
-            }
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
-                if (more) issue4(ks + 1, buf ^ 1, 4 * kk);
-#pragma unroll
-                for (int a2 = 0; a2 < 2; ++a2)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        acc[a2][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[kk][a2], bh[kk][b], acc[a2][b], 0, 0, 0);
-                        acc[a2][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk][a2], bl[kk][b], acc[a2][b], 0, 0, 0);
-                        acc[a2][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk][a2], bh[kk][b], acc[a2][b], 0, 0, 0);
-                    }
-            }
-        }
-    } else {
+    // (Measured and removed in round 4: requesting both k-steps' fragments of a stage at once,
+    // two register sets, 250 VGPRs: B = 64 NS Gram 200 -> 205 us, stress 277 -> 285;
+    // profiles/r03y_d2_fp16_ab.txt.)
+    {
         for (int ks = 0; ks < nks; ++ks) {
             const int buf = ks & 1;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's stage-ks DMAs
@@ -1890,20 +1842,11 @@ __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict_
             }
         }
     }
-    if (diag_epi == 1) {   // GLL_GRAM_DIAG = 1 (timing diagnostic): no epilogue, D2 as it was
-        float s = 0.f;
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) s += acc[a][b][0];
-        if (s == 1234.5f) D2[0] = s;   // keeps the MFMAs alive
-        return;
-    }
     // epilogue: D2 = |a_i|^2 + |a_j|^2 - 2 <a_i, a_j>; C layout of 32x32: col = lane & 31,
     // row = (e & 3) + 8 (e >> 2) + 4 h.  Diagonal tiles keep the upper triangle (tj >= ti, the
     // value gram_pk_kernel stores there) and write it in both orientations.
     const bool diag = bi == bj;
-    if (!diag && diag_epi == 0) {
+    if (!diag) {
         // Off-diagonal tiles (round 3): the mirrored orientation leaves the registers as one
         // 16-B store per lane (a lane holds 4 consecutive rows of its column), while the direct
         // one -- 128 four-byte stores per wave, 256 B each -- goes through LDS: each half of the
@@ -2024,19 +1967,12 @@ __global__ __launch_bounds__(512) void gram_pk2_kernel(const __bf16* __restrict_
 // 256-tiles (gram_pk2_kernel) or 128-tiles (gram_pk_kernel) for the pre-split GEMM: the one
 // with fewer waves of one-workgroup-per-CU rounds x k-stage bytes (a round of 256-tiles moves
 // the same 64 KiB per stage as one of 128-tiles but does 4x the work, in twice the stages).
-// GLL_GRAM_TILE = 128 / 256 forces one (diagnostic A/B).
+// The knob GLL_KNOB_GRAM_TILE = 128 / 256 forces one (tests).
 static bool gram_tile256(const Layout& L, const Batch& bt, int T, int T2) {
-    const char* e = getenv("GLL_GRAM_TILE");
-    if (e) return atoi(e) == 256;
+    if (knob(GLL_KNOB_GRAM_TILE) > 0) return knob(GLL_KNOB_GRAM_TILE) == 256 && L.dp % kPK2 == 0;
     // (d <= 128: a tile is 4 k-stages; the FullySup shape measured 225 -> 230 us at B = 64)
     if (L.dp % kPK2 || L.dp <= 128) return false;
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, v = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
-        cus = v > 0 ? v : 256;
-    }
+    const int cus = device_cus();
     const int64_t t1 = int64_t(bt.B) * T * (T + 1) / 2, t2 = int64_t(bt.B) * T2 * (T2 + 1) / 2;
     const int64_t r1 = (t1 + cus - 1) / cus, r2 = (t2 + cus - 1) / cus;
     return r2 * 2 * (L.dp / kPK2) * kPK2 < r1 * (L.dp / kPK) * kPK;   // stage bytes equal
@@ -2046,16 +1982,14 @@ static bool gram_tile256(const Layout& L, const Batch& bt, int T, int T2) {
 // and n <= 12,288 (see launch_gram).  Its D2 is stored fp16 (dput) unless GLL_D2_F32 = 1 (A/B).
 static bool presplit_route(const Layout& L, const Batch& bt) {
     const int T = (L.n + 127) / 128;
-    return !(L.flags & GLL_FLAG_GRAM_NARROW) && int64_t(bt.B) * T * (T + 1) / 2 >= 256 &&
+    return int64_t(bt.B) * T * (T + 1) / 2 >= 256 &&
            !(L.flags & GLL_FLAG_GRAM_INLINE) && (bt.B > 1 || (L.d > 128 && L.n <= 12288)) &&
            gram_planes(L, bt.B) == 1 && L.PR == L.n;
 }
-// Batches only (GLL_D2_HALF1 = 1 extends it to single graphs for A/B): see DESIGN.md §3.1 and
-// profiles/r03x_d2_fp16_ab.txt.
+// Batches only (single graphs measured slower with it: at stress the wider candidate margin
+// cost the select 274 -> 299 us; DESIGN.md §3.1, profiles/r03x_d2_fp16_ab.txt).
 static bool d2_half(const Layout& L, const Batch& bt) {
-    static const bool f32 = getenv("GLL_D2_F32") && atoi(getenv("GLL_D2_F32")) != 0;
-    static const bool one = getenv("GLL_D2_HALF1") && atoi(getenv("GLL_D2_HALF1")) != 0;  // A/B
-    return !f32 && !(L.flags & GLL_FLAG_D2_F32) && (bt.B > 1 || one) && presplit_route(L, bt);
+    return !(L.flags & GLL_FLAG_D2_F32) && bt.B > 1 && presplit_route(L, bt);
 }
 
 hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
@@ -2103,13 +2037,10 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
             launch_k(gram_split_kernel<false>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
         const bool H = d2_half(L, bt);
         const int T2 = (L.n + 255) / 256;
-        static const int gram_diag = getenv("GLL_GRAM_DIAG") ? atoi(getenv("GLL_GRAM_DIAG")) : 0;
-        static const bool gram_pipe = getenv("GLL_GRAM_PIPE") && atoi(getenv("GLL_GRAM_PIPE")) != 0;
         if (gram_tile256(L, bt, T, T2))
-            launch_k(H ? (gram_pipe ? gram_pk2_kernel<true, true> : gram_pk2_kernel<true, false>)
-                       : (gram_pipe ? gram_pk2_kernel<false, true> : gram_pk2_kernel<false, false>),
+            launch_k(H ? gram_pk2_kernel<true> : gram_pk2_kernel<false>,
                      dim3(unsigned(bt.B * T2 * (T2 + 1) / 2)), 512, 0, s, Ph, Pl, nrm, L.n, L.dp,
-                     T2, D2, L.ldD, bt.ws, gram_diag, d2s);
+                     T2, D2, L.ldD, bt.ws, d2s);
         else
             launch_k(H ? gram_pk_kernel<true> : gram_pk_kernel<false>,
                      dim3(unsigned(bt.B * T * (T + 1) / 2)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T,
@@ -2117,7 +2048,7 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         prof_end(GLL_K_GRAM, s);
         return launch_status("knn.hip:launch_gram(pk)");
     }
-    if (!(L.flags & GLL_FLAG_GRAM_NARROW) && int64_t(bt.B) * T * (T + 1) / 2 >= 512) {
+    if (int64_t(bt.B) * T * (T + 1) / 2 >= 512) {
         const dim3 grid(T * (T + 1) / 2, bt.B);
         prof_begin(GLL_K_GRAM, s);
         if (vec)
@@ -2173,8 +2104,6 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     if (margin > 8) margin = 8;
     int kc = K - 1 + margin;
     if (kc > n - 1) kc = n - 1;
-    static const int hold = getenv("GLL_SEL_HOLD") ? atoi(getenv("GLL_SEL_HOLD")) : 1;  // A/B
-    static const int diag = getenv("GLL_SEL_DIAG") ? atoi(getenv("GLL_SEL_DIAG")) : 0;
     const size_t plane = size_t(n) * L.ldD;
     const int planes = gram_planes(L, bt.B);
     dim3 grid((rows + 3) / 4, bt.B);
@@ -2196,7 +2125,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
         L.RCAP,                                                                                \
         L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \
         L.at<int32_t>(ws, L.rev_cnt), L.at<int32_t>(ws, L.rev_idx), L.at<float>(ws, L.rev_d2), \
-        L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub, bt.x, bt.ws, bt.st, diag, \
+        L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub, bt.x, bt.ws, bt.st,       \
         r0, r0 + rows, d2s)
 #define GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, CHV)                                              \
     do {                                                                                       \
@@ -2206,8 +2135,8 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
 // the threshold scan holds rows of <= 2048 columns in registers (KC <= 32, aligned d)
 #define GLL_SEL4(KCV, V, NPV, NUS, NUB, XQV)                                                   \
     do {                                                                                       \
-        if (KCV <= 32 && V && hold && n <= 1024 && rows == n) GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, (KCV <= 32 && V ? 1 : 0)); \
-        else if (KCV <= 32 && V && hold && n <= 2048 && rows == n) GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, (KCV <= 32 && V ? 2 : 0)); \
+        if (KCV <= 32 && V && n <= 1024 && rows == n) GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, (KCV <= 32 && V ? 1 : 0)); \
+        else if (KCV <= 32 && V && n <= 2048 && rows == n) GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, (KCV <= 32 && V ? 2 : 0)); \
         else GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, 0);                                          \
     } while (0)
 #define GLL_SEL(KCV, V)                                                                        \

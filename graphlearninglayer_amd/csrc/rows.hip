@@ -325,6 +325,7 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
     if (i == 0 && lane == 0) {   // the backward's hand-off counters start at zero
         a.fsync[0] = 0u;
         a.fsync[32] = 0u;
+        a.fsync[64] = 0u;   // a poisoned workspace (lost solve) is rebuilt here
     }
     const int Km1 = a.K - 1;
     int fi = -1;

@@ -190,9 +190,10 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int& total) 
     }
 }
 
-// MODE: 3 Chronopoulos-Gear with a first-order Neumann preconditioner (below; the default),
-// 0 classic PCG (two reductions), 1 Chronopoulos-Gear (one reduction, two barriers),
-// 2 pipelined PCG (Ghysels-Vanroose: one barrier per iteration).
+// MODE: 3 Chronopoulos-Gear with a first-order Neumann preconditioner (below; the default where
+// a thread owns one row), 1 Chronopoulos-Gear (one reduction, two barriers per iteration).
+// (Measured and removed in round 4, DESIGN.md §3.2: the classic two-reduction form and the
+// pipelined Ghysels-Vanroose form.)
 // The kernel body: `gxy` = (column, graph); `fsync` (the fused backward, cg_grad_fused_kernel)
 // non-null: the solution is stored write-through (sc1) and, once every wave has drained its
 // stores, thread 0 adds 1 to fsync[0] -- the feature-gradient workgroups of the same launch
@@ -227,8 +228,8 @@ __device__ __forceinline__ void cg_ell_body(
     float* red = smem;                                  // 96 floats of reduction scratch
     int* scan = reinterpret_cast<int*>(smem + 96);      // 16 ints of scan scratch
     const int mp4 = (m + 3) & ~3;
-    float* P_ = smem + 128;                             // gathered vector (x2 when pipelined)
-    int* lcol = reinterpret_cast<int*>(P_ + (MODE >= 2 ? 2 : 1) * mp4);   // overflow, compacted
+    float* P_ = smem + 128;                             // gathered vector (x2 for MODE 3)
+    int* lcol = reinterpret_cast<int*>(P_ + (MODE == 3 ? 2 : 1) * mp4);   // overflow, compacted
     float* lw = reinterpret_cast<float*>(lcol + mat_cap);
     // (Ordering rows by length so each wave's slot bound tracks its own rows was measured:
     // no gain per iteration at NS, +1.5 us of setup from the permuted ELL loads.)
@@ -323,7 +324,8 @@ __device__ __forceinline__ void cg_ell_body(
     if constexpr (NT > kWave) __syncthreads();
     int it = 0;
     bool conv;
-    if constexpr (MODE != 0) {
+    static_assert(MODE == 1 || MODE == 3, "MODE: 1 Chronopoulos-Gear, 3 with Neumann-1");
+    {
         // Each wave gathers only the ELL slots some row of its own holds (wave-uniform bound
         // in groups of 4: rows average ~6 of the 24 slots at NS).
         int smax[R];
@@ -383,7 +385,7 @@ __device__ __forceinline__ void cg_ell_body(
             }
             return dg[q] * pq - acc;   // (Luu u)_row = (deg + tau) u_row - sum_j W_rowj u_j
         };
-        if constexpr (MODE == 1 || MODE == 3) {
+        {
         // Chronopoulos-Gear single-reduction PCG: one fused (r.u, w.u, r.r) exchange and one
         // publish barrier per iteration (classic PCG: two exchanges + publish = 3 barriers).
         // s = A p by recurrence; u = M^-1 r is what is published and multiplied.
@@ -494,176 +496,7 @@ __device__ __forceinline__ void cg_ell_body(
             }
             GLL_TRACE_CYC(15);
         }
-        } else {
-        // Pipelined PCG (Ghysels & Vanroose 2014, preconditioned form): m = M^-1 w and n = A m
-        // by recurrence-free products, z, q, s, p by recurrences.  The reduction of
-        // (r,u), (w,u), (r,r) and the SpMV of m do not depend on each other, so one barrier
-        // per iteration publishes both; the LDS totals are read while the gathers are in
-        // flight.  The gathered vector is double-buffered: a fast wave may publish m_{i+1}
-        // while a slow one still gathers m_i.
-        float* Pb0 = P_;
-        float* Pb1 = P_ + mp4;
-        float w[R], z[R], qv[R], sv[R], mv[R];
-        float gl = 0.f, dl = 0.f, rl = 0.f;
-#pragma unroll
-        for (int q = 0; q < R; ++q) {
-            ap[q] = p[q];                      // u0 = M^-1 r0, published in Pb0 above
-            p[q] = z[q] = qv[q] = sv[q] = 0.f;
-            w[q] = spmv(q, ap[q], Pb0);        // w0 = A u0
-            mv[q] = mi[q] * w[q];
-            const int u = urow[q];
-            if (u < m) Pb1[u] = mv[q];
-            gl += r[q] * ap[q];
-            dl += w[q] * ap[q];
-            rl += r[q] * r[q];
         }
-        GLL_TRACE_PT(3);
-        const float* qred = block_sum3_post<NT>(gl, dl, rl, red, phase);
-        int cur = 1;
-        float tol2 = 0.f, gam = 0.f, alpha = 0.f;
-        conv = false;
-        while (true) {
-            GLL_TRACE_CYC(10);
-            block_sum3_read<NT>(qred, gl, dl, rl);   // gamma_i, delta_i, |r_i|^2
-            const float* Pc = cur ? Pb1 : Pb0;
-            float nv[R];
-#pragma unroll
-            for (int q = 0; q < R; ++q) nv[q] = spmv(q, mv[q], Pc);   // n_i = A m_i
-            GLL_TRACE_CYC(11);
-            if (it == 0) {
-                tol2 = rtol * rtol * rl;
-                if (!(rl > 0.f)) {
-                    conv = true;
-                    break;
-                }
-            } else if (rl <= tol2) {
-                conv = true;
-                break;
-            }
-            if (it >= max_iter) break;
-            float beta, a;
-            if (it == 0) {
-                if (!(dl > 0.f)) break;   // breakdown before the first step
-                beta = 0.f;
-                a = gl / dl;
-            } else {
-                beta = gl * __builtin_amdgcn_rcpf(gam);
-                const float den = alpha * dl - beta * gl;
-                if (!(den > 0.f)) break;   // breakdown or NaN: reported as non-converged
-                a = (gl * alpha) * __builtin_amdgcn_rcpf(den);
-            }
-            ++it;
-            gam = gl;
-            alpha = a;
-            float* Pn = cur ? Pb0 : Pb1;
-            gl = dl = rl = 0.f;
-#pragma unroll
-            for (int q = 0; q < R; ++q) {
-                z[q] = nv[q] + beta * z[q];
-                qv[q] = mv[q] + beta * qv[q];
-                sv[q] = w[q] + beta * sv[q];
-                p[q] = ap[q] + beta * p[q];
-                x[q] += a * p[q];
-                r[q] -= a * sv[q];
-                ap[q] -= a * qv[q];
-                w[q] -= a * z[q];
-                mv[q] = mi[q] * w[q];
-                const int u = urow[q];
-                if (u < m) Pn[u] = mv[q];
-                gl += r[q] * ap[q];
-                dl += w[q] * ap[q];
-                rl += r[q] * r[q];
-            }
-            GLL_TRACE_CYC(12);
-            qred = block_sum3_post<NT>(gl, dl, rl, red, phase);
-            cur ^= 1;
-            GLL_TRACE_CYC(13);
-        }
-        }
-    } else {
-    block_sum2<NT>(rz, bb, red, phase);
-    GLL_TRACE_PT(3);
-    const float tol2 = rtol * rtol * bb;
-    conv = !(bb > 0.f);
-    while (!conv && it < max_iter) {
-        ++it;
-        float pap = 0.f, unused = 0.f;
-#pragma unroll
-        for (int q = 0; q < R; ++q) {
-            float acc = 0.f;
-#pragma unroll
-            for (int s = 0; s < S; ++s)
-                acc += ew[q][s] * P_[ec[q][s]];
-            if (matl) {
-                // four entries per step, every LDS read issued before use (same summation
-                // order as one at a time); rows past the slots are long at K = 25
-                const int e0 = ost[q], no = olen[q];
-                int t = 0;
-                for (; t + 4 <= no; t += 4) {
-                    int c4[4];
-                    float w4[4], p4[4];
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        c4[v] = lcol[e0 + t + v];
-                        w4[v] = lw[e0 + t + v];
-                    }
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) p4[v] = P_[c4[v]];
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) acc += w4[v] * p4[v];
-                }
-                for (; t < no; ++t) acc += lw[e0 + t] * P_[lcol[e0 + t]];
-            } else {   // from the CSR (L2), four entries in flight per step
-                const int e0 = ost[q], no = olen[q];
-                int t = 0;
-                for (; t + 4 <= no; t += 4) {
-                    int c4[4];
-                    float w4[4], p4[4];
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        c4[v] = col[e0 + t + v];
-                        w4[v] = wv[e0 + t + v];
-                    }
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) p4[v] = P_[c4[v] - base];
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) acc += w4[v] * p4[v];
-                }
-                for (; t < no; ++t) acc += wv[e0 + t] * P_[col[e0 + t] - base];
-            }
-            ap[q] = dg[q] * p[q] - acc;   // (Luu p)_u = (deg_u + tau) p_u - sum_j W_uj p_j
-            pap += p[q] * ap[q];
-        }
-        if (it == 1) GLL_TRACE_PT(4);
-        block_sum2<NT>(pap, unused, red, phase);
-        if (it == 1) GLL_TRACE_PT(5);
-        if (!(pap > 0.f)) break;   // breakdown or NaN: stop, reported as non-converged
-        const float alpha = rz / pap;
-        float rr = 0.f, rzn = 0.f;
-#pragma unroll
-        for (int q = 0; q < R; ++q) {
-            x[q] += alpha * p[q];
-            r[q] -= alpha * ap[q];
-            rr += r[q] * r[q];
-            rzn += r[q] * mi[q] * r[q];
-        }
-        block_sum2<NT>(rr, rzn, red, phase);
-        if (it == 1) GLL_TRACE_PT(6);
-        if (rr <= tol2) {
-            conv = true;
-            break;
-        }
-        const float beta = rzn / rz;
-        rz = rzn;
-#pragma unroll
-        for (int q = 0; q < R; ++q) {
-            p[q] = mi[q] * r[q] + beta * p[q];
-            const int u = urow[q];
-            if (u < m) P_[u] = p[q];
-        }
-        if constexpr (NT > kWave) __syncthreads();
-        if (it == 1) GLL_TRACE_PT(7);
-    }
     }
     GLL_TRACE_PT(8);
 #pragma unroll
@@ -708,386 +541,6 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
                                     ucnt, col, wv, diag, bsrc, out64, out32, rtol, max_iter,
                                     mat_cap, st_nonconv, st_iters, ell_col, ell_w, wss, bs, us,
                                     sts);
-}
-
-// --------------------------------------------------------------------------------------
-// Column-pair CG for batches (cg_ell2_kernel, round 3): NC right-hand-side columns of one graph
-// per workgroup, the Chronopoulos-Gear recurrences of cg_ell_body MODE 1 run per column.
-// Batched launches are throughput-bound: B x C workgroups of the one-column kernel hold the
-// same ELL slices in registers C times over and issue one 4-B LDS gather per entry and column.
-// Here the published vectors are interleaved ([u][NC] floats), so one gather of NC x 4 B serves
-// every column, the ELL slice is loaded and held once per NC columns, and the NC columns' three
-// dot products share one LDS exchange and barrier.  Each column keeps its own step sizes,
-// convergence test and iteration count; a finished column is frozen (its x never changes
-// again) while the others go on.  Per column the arithmetic -- slot order, the DPP and LDS
-// reduction order, the recurrences -- is cg_ell_body MODE 1's, so the solutions are those of
-// the one-column kernel to fp32 contraction order.  Measured slower (B = 64 NS 21.6 -> 27.6 us
-// per launch, profiles/r03s_cg_pairs_ab.txt): the batched solve is bound by each workgroup's iteration
-// latency, not by the gathers and loads it saves, so it stays a diagnostic (GLL_FLAG_CG_PAIRS).
-// --------------------------------------------------------------------------------------
-template <int NT, int N>
-__device__ __forceinline__ void block_sumN(float (&v)[N], float* red, int& phase) {
-#pragma unroll
-    for (int k = 0; k < N; ++k) v[k] = dpp_add<0xB1, 0xf>(v[k]);
-#pragma unroll
-    for (int k = 0; k < N; ++k) v[k] = dpp_add<0x4E, 0xf>(v[k]);
-#pragma unroll
-    for (int k = 0; k < N; ++k) v[k] = dpp_add<0x141, 0xf>(v[k]);
-#pragma unroll
-    for (int k = 0; k < N; ++k) v[k] = dpp_add<0x140, 0xf>(v[k]);
-#pragma unroll
-    for (int k = 0; k < N; ++k) v[k] = dpp_add<0x142, 0xa>(v[k]);
-#pragma unroll
-    for (int k = 0; k < N; ++k) v[k] = dpp_add<0x143, 0xc>(v[k]);
-    constexpr int NW = NT / kWave;
-    constexpr int NQ = NW < 4 ? 4 : NW;
-    float* q = red + phase * N * NQ;
-    phase ^= 1;
-    if (lane_id() == 63) {
-        const int w = threadIdx.x >> 6;
-#pragma unroll
-        for (int k = 0; k < N; ++k) q[k * NQ + w] = v[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-        float a = 0.f;
-        if constexpr (NW % 4 == 0) {
-#pragma unroll
-            for (int w = 0; w < NW; w += 4) {
-                const f32x4 va = *reinterpret_cast<const f32x4*>(q + k * NQ + w);
-                a += va.x; a += va.y; a += va.z; a += va.w;
-            }
-        } else {
-#pragma unroll
-            for (int w = 0; w < NW; ++w) a += q[k * NQ + w];
-        }
-        v[k] = a;
-    }
-}
-
-template <int NC>
-struct vecN { using type = float; };
-template <>
-struct vecN<2> { using type = f32x2; };
-template <>
-struct vecN<4> { using type = f32x4; };
-
-template <int NT, int R, int S, typename TB, int NC>
-__global__ __launch_bounds__(NT) void cg_ell2_kernel(
-    int m, int C, int base, const int32_t* __restrict__ row_start,
-    const int32_t* __restrict__ row_len, const int32_t* __restrict__ ucnt,
-    const int32_t* __restrict__ col, const float* __restrict__ wv, const float* __restrict__ diag,
-    const TB* __restrict__ bsrc, double* __restrict__ out64, float* __restrict__ out32,
-    float rtol, int max_iter, int mat_cap, int32_t* __restrict__ st_nonconv,
-    int32_t* __restrict__ st_iters, const int32_t* __restrict__ ell_col,
-    const float* __restrict__ ell_w, size_t wss, size_t bs, size_t us, size_t sts) {
-    static_assert(NT > kWave, "block reductions assume several waves");
-    using VT = typename vecN<NC>::type;
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int2 gxy = batch_xy<true>();
-    ell_col = gshift_at(ell_col, wss, gxy.y);
-    ell_w = gshift_at(ell_w, wss, gxy.y);
-    row_start = gshift_br_at(row_start, wss, gxy.y);
-    row_len = gshift_br_at(row_len, wss, gxy.y);
-    ucnt = gshift_at(ucnt, wss, gxy.y);
-    col = gshift_br_at(col, wss, gxy.y);
-    wv = gshift_br_at(wv, wss, gxy.y);
-    diag = gshift_at(diag, wss, gxy.y);
-    bsrc = gshift_at(bsrc, bs, gxy.y);
-    out64 = gshift_br_at(out64, us, gxy.y);
-    out32 = gshift_br_at(out32, wss, gxy.y);
-    st_nonconv = gshift_br_at(st_nonconv, sts, gxy.y);
-    st_iters = gshift_br_at(st_iters, sts, gxy.y);
-    const int c0 = gxy.x * NC;
-    const int tid = threadIdx.x;
-    float* red = smem;                                     // 2 x 3NC x 4+ floats of reduction
-    int* scan = reinterpret_cast<int*>(smem + 2 * 3 * NC * 8);   // 16 ints of scan scratch
-    VT* P_ = reinterpret_cast<VT*>(smem + 2 * 3 * NC * 8 + 16);  // published u, [u][NC]
-    const int mp4 = (m + 3) & ~3;
-    int* lcol = reinterpret_cast<int*>(P_ + mp4);          // overflow entries, compacted
-    float* lw = reinterpret_cast<float*>(lcol + mat_cap);
-    int urow[R];
-#pragma unroll
-    for (int q = 0; q < R; ++q) urow[q] = tid + NT * q;
-    int ec[R][S];
-    float ew[R][S];
-    int ost[R], olen[R], ulen[R];
-    float dg[R], mi[R];
-    float x[R][NC], r[R][NC], p[R][NC], sv[R][NC], bv[R][NC];
-    int tov = 0;
-#pragma unroll
-    for (int q = 0; q < R; ++q) {
-        const int u = urow[q];
-        const int uc = u < m ? u : 0;
-        ulen[q] = ucnt[uc];
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            ec[q][s] = ell_col[size_t(s) * m + uc];
-            ew[q][s] = ell_w[size_t(s) * m + uc];
-        }
-        dg[q] = diag[uc];
-#pragma unroll
-        for (int k = 0; k < NC; ++k)
-            bv[q][k] = c0 + k < C ? to_f32(bsrc[size_t(uc) * C + c0 + k]) : 0.f;
-    }
-    int longer = 0;
-#pragma unroll
-    for (int q = 0; q < R; ++q) {
-        if (urow[q] >= m) ulen[q] = 0;
-        longer |= ulen[q] > S ? 1 : 0;
-    }
-    const bool has_ovf = __syncthreads_or(longer) != 0;
-    float rz[NC], bb[NC];
-#pragma unroll
-    for (int k = 0; k < NC; ++k) rz[k] = bb[k] = 0.f;
-#pragma unroll
-    for (int q = 0; q < R; ++q) {
-        const int u = urow[q];
-        if (u >= m) {
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                ec[q][s] = 0;
-                ew[q][s] = 0.f;
-            }
-            dg[q] = 0.f;
-        }
-        ost[q] = 0;
-        olen[q] = 0;
-        if (has_ovf && u < m) {
-            const int len = ulen[q];
-            ost[q] = row_start[base + u] + row_len[base + u] - len + S;
-            olen[q] = len - S;
-            tov += olen[q] > 0 ? olen[q] : 0;
-        }
-        mi[q] = 0.f;
-        VT pv;
-#pragma unroll
-        for (int k = 0; k < NC; ++k) {
-            x[q][k] = r[q][k] = p[q][k] = sv[q][k] = 0.f;
-        }
-        if (u < m) {
-            mi[q] = dg[q] > 0.f ? 1.f / dg[q] : 0.f;
-#pragma unroll
-            for (int k = 0; k < NC; ++k) {
-                r[q][k] = mi[q] > 0.f ? bv[q][k] : 0.f;
-                p[q][k] = mi[q] * r[q][k];
-                rz[k] += r[q][k] * p[q][k];
-                bb[k] += r[q][k] * r[q][k];
-            }
-        }
-        if constexpr (NC == 1) pv = p[q][0];
-        else {
-#pragma unroll
-            for (int k = 0; k < NC; ++k) pv[k] = p[q][k];
-        }
-        if (u < m) P_[u] = pv;
-    }
-    int ov_total = 0;
-    int ooff = has_ovf ? block_excl_scan<NT>(tov, scan, ov_total) : 0;
-    const bool matl = ov_total <= mat_cap;
-    if (has_ovf && matl) {
-#pragma unroll
-        for (int q = 0; q < R; ++q) {
-            for (int t = 0; t < olen[q]; ++t) {
-                const int e = ost[q] + t;
-                lcol[ooff + t] = col[e] - base;
-                lw[ooff + t] = wv[e];
-            }
-            if (olen[q] > 0) {
-                ost[q] = ooff;
-                ooff += olen[q];
-            }
-        }
-    }
-    int phase = 0;
-    __syncthreads();
-    int smax[R];
-#pragma unroll
-    for (int q = 0; q < R; ++q) smax[q] = wave_max_int(ulen[q] < S ? ulen[q] : S);
-    // (A y)_row for every column: diag y_row - sum W y_j, the one-column kernel's slot order
-    auto spmv = [&](int q, const float (&yq)[NC], float (&out)[NC]) {
-        VT pv[S];
-#pragma unroll
-        for (int s0 = 0; s0 < S; s0 += 4) {
-            if (s0 < smax[q]) {
-#pragma unroll
-                for (int t = 0; t < 4 && s0 + t < S; ++t) pv[s0 + t] = P_[ec[q][s0 + t]];
-            } else {
-#pragma unroll
-                for (int t = 0; t < 4 && s0 + t < S; ++t) pv[s0 + t] = VT{};
-            }
-        }
-        float acc[NC];
-#pragma unroll
-        for (int k = 0; k < NC; ++k) acc[k] = 0.f;
-        auto add = [&](float wgt, VT v) {
-            if constexpr (NC == 1) acc[0] += wgt * v;
-            else {
-#pragma unroll
-                for (int k = 0; k < NC; ++k) acc[k] += wgt * v[k];
-            }
-        };
-#pragma unroll
-        for (int s2 = 0; s2 < S; ++s2) add(ew[q][s2], pv[s2]);
-        const int e0 = ost[q], no = olen[q];
-        if (matl) {
-            int t = 0;
-            for (; t + 4 <= no; t += 4) {
-                int c4[4];
-                float w4[4];
-                VT p4[4];
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    c4[v] = lcol[e0 + t + v];
-                    w4[v] = lw[e0 + t + v];
-                }
-#pragma unroll
-                for (int v = 0; v < 4; ++v) p4[v] = P_[c4[v]];
-#pragma unroll
-                for (int v = 0; v < 4; ++v) add(w4[v], p4[v]);
-            }
-            for (; t < no; ++t) add(lw[e0 + t], P_[lcol[e0 + t]]);
-        } else {
-            int t = 0;
-            for (; t + 4 <= no; t += 4) {
-                int c4[4];
-                float w4[4];
-                VT p4[4];
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    c4[v] = col[e0 + t + v];
-                    w4[v] = wv[e0 + t + v];
-                }
-#pragma unroll
-                for (int v = 0; v < 4; ++v) p4[v] = P_[c4[v] - base];
-#pragma unroll
-                for (int v = 0; v < 4; ++v) add(w4[v], p4[v]);
-            }
-            for (; t < no; ++t) add(wv[e0 + t], P_[col[e0 + t] - base]);
-        }
-#pragma unroll
-        for (int k = 0; k < NC; ++k) out[k] = dg[q] * yq[k] - acc[k];
-    };
-    // pre-step: s0 = A u0 (u0 = p, published), gamma0 = (r,u), delta0 = (s,u)
-    float tot[3 * NC];
-    {
-        float dl[NC];
-#pragma unroll
-        for (int k = 0; k < NC; ++k) dl[k] = 0.f;
-#pragma unroll
-        for (int q = 0; q < R; ++q) {
-            spmv(q, p[q], sv[q]);
-#pragma unroll
-            for (int k = 0; k < NC; ++k) dl[k] += p[q][k] * sv[q][k];
-        }
-#pragma unroll
-        for (int k = 0; k < NC; ++k) {
-            tot[3 * k] = rz[k];
-            tot[3 * k + 1] = bb[k];
-            tot[3 * k + 2] = dl[k];
-        }
-    }
-    block_sumN<NT, 3 * NC>(tot, red, phase);
-    float tol2[NC], gam[NC], alpha[NC];
-    bool act[NC], conv[NC];
-    int it[NC];
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-        const float bbk = tot[3 * k + 1], dlk = tot[3 * k + 2];
-        tol2[k] = rtol * rtol * bbk;
-        conv[k] = !(bbk > 0.f);
-        gam[k] = tot[3 * k];
-        alpha[k] = dlk > 0.f ? gam[k] / dlk : 0.f;
-        if (!(dlk > 0.f)) alpha[k] = -1.f;
-        it[k] = 0;
-        act[k] = !conv[k] && alpha[k] > 0.f && it[k] < max_iter;
-    }
-    bool any = false;
-#pragma unroll
-    for (int k = 0; k < NC; ++k) any |= act[k];
-    while (any) {
-        float ap[R][NC];
-#pragma unroll
-        for (int k = 0; k < NC; ++k) it[k] += act[k] ? 1 : 0;
-#pragma unroll
-        for (int q = 0; q < R; ++q) {
-            VT pv;
-#pragma unroll
-            for (int k = 0; k < NC; ++k) {
-                if (act[k]) {
-                    x[q][k] += alpha[k] * p[q][k];
-                    r[q][k] -= alpha[k] * sv[q][k];
-                }
-                ap[q][k] = act[k] ? mi[q] * r[q][k] : 0.f;
-                if constexpr (NC == 1) pv = ap[q][0];
-                else pv[k] = ap[q][k];
-            }
-            const int u = urow[q];
-            if (u < m) P_[u] = pv;
-        }
-        __syncthreads();
-        float w[R][NC];
-#pragma unroll
-        for (int k = 0; k < 3 * NC; ++k) tot[k] = 0.f;
-#pragma unroll
-        for (int q = 0; q < R; ++q) {
-            spmv(q, ap[q], w[q]);
-#pragma unroll
-            for (int k = 0; k < NC; ++k) {
-                tot[3 * k] += r[q][k] * ap[q][k];
-                tot[3 * k + 1] += w[q][k] * ap[q][k];
-                tot[3 * k + 2] += r[q][k] * r[q][k];
-            }
-        }
-        block_sumN<NT, 3 * NC>(tot, red, phase);
-        any = false;
-#pragma unroll
-        for (int k = 0; k < NC; ++k) {
-            if (!act[k]) continue;
-            const float gn = tot[3 * k], de = tot[3 * k + 1], rr = tot[3 * k + 2];
-            if (rr <= tol2[k]) {
-                conv[k] = true;
-                act[k] = false;
-                continue;
-            }
-            const float beta = gn * __builtin_amdgcn_rcpf(gam[k]);
-            const float den = alpha[k] * de - beta * gn;
-            if (!(den > 0.f)) {   // breakdown or NaN: reported as non-converged
-                act[k] = false;
-                continue;
-            }
-            alpha[k] = (gn * alpha[k]) * __builtin_amdgcn_rcpf(den);
-            gam[k] = gn;
-#pragma unroll
-            for (int q = 0; q < R; ++q) {
-                p[q][k] = ap[q][k] + beta * p[q][k];
-                sv[q][k] = w[q][k] + beta * sv[q][k];
-            }
-            act[k] = it[k] < max_iter && alpha[k] > 0.f;
-            any |= act[k];
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < R; ++q) {
-        const int u = urow[q];
-        if (u < m) {
-#pragma unroll
-            for (int k = 0; k < NC; ++k) {
-                if (c0 + k >= C) continue;
-                if (out64) out64[size_t(u) * C + c0 + k] = double(x[q][k]);
-                if (out32) out32[size_t(u) * C + c0 + k] = x[q][k];
-            }
-        }
-    }
-    if (tid == 0) {
-#pragma unroll
-        for (int k = 0; k < NC; ++k) {
-            if (c0 + k >= C) continue;
-            if (st_iters) atomicMax(st_iters, it[k]);
-            if (!conv[k] && st_nonconv) atomicAdd(st_nonconv, 1);
-        }
-    }
 }
 
 // --------------------------------------------------------------------------------------
@@ -1491,27 +944,19 @@ template <int NT, int R, int S, typename TB, int MODE>
 static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* b, size_t bs,
                           double* out64, float* out32, float rtol, int max_iter,
                           int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
-    size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4 * (MODE >= 2 ? 2 : 1);
+    size_t lds = 128 * 4 + size_t((L.m + 3) & ~3) * 4 * (MODE == 3 ? 2 : 1);
     // entries past the ELL slices are compacted into LDS up to kOvfLds of them, the rest read
     // from the CSR; batched launches cap them so 4 workgroups still share a CU (a full-LDS
     // request would pin one per CU); a single graph's C workgroups take all the LDS there is
     // (K = 25 rows overflow 16 slots by ~14K entries at m = 1250)
     const int64_t kOvfLds = bt.B == 1 ? int64_t(1) << 30 : 2048;
-    static const char* pad_env = getenv("GLL_CG_LDS_PAD");   // diagnostic: bytes of LDS per
-    const size_t lds_pad = pad_env ? size_t(atoi(pad_env)) : 0;   // workgroup at least
     const int64_t eu_bound = int64_t(L.m + L.n) * (L.K - 1);
     int64_t cap = int64_t(kLdsDyn - lds) / 8;
     if (cap > eu_bound) cap = eu_bound;
     if (cap > kOvfLds) cap = kOvfLds;
     if (cap < 0) cap = 0;
     lds += size_t(cap) * 8;
-    if (lds < lds_pad) lds = lds_pad;
-    if (S != ell_emit(L, bt.B)) {   // row_build emitted ell_emit(L, B) slots
-        (void)hipGetLastError();
-        if (getenv("GLL_DEBUG"))
-            fprintf(stderr, "gll: run_ell S=%d but ELL width %d\n", S, ell_emit(L, bt.B));
-        return hipErrorInvalidValue;
-    }
+    if (S != ell_emit(L, bt.B)) return hipErrorInvalidValue;   // row_build emitted ell_emit(L, B)
     auto fn = cg_ell_kernel<NT, R, S, TB, MODE>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
     launch_k(fn, dim3(L.C, bt.B), NT, lds, s, 
@@ -1520,33 +965,6 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
         L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, int(cap), st_nonconv, st_iters,
         L.at<int32_t>(ws, L.ell_col), L.at<float>(ws, L.ell_w), bt.ws, bs, bt.u, bt.st);
     return launch_status("solve.hip:run_ell");
-}
-
-template <int NT, int R, int S, typename TB, int NC>
-static hipError_t run_ell2(const Layout& L, const Batch& bt, void* ws, const TB* b, size_t bs,
-                           double* out64, float* out32, float rtol, int max_iter,
-                           int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
-    static_assert(NT <= 512, "reduction scratch sized for <= 8 waves");
-    size_t lds = size_t(2 * 3 * NC * 8 + 16) * 4 + size_t((L.m + 3) & ~3) * 4 * NC;
-    // overflow entries as run_ell caps them for batches (2048: several workgroups per CU)
-    const int64_t eu_bound = int64_t(L.m + L.n) * (L.K - 1);
-    int64_t cap = int64_t(kLdsDyn - lds) / 8;
-    if (cap > eu_bound) cap = eu_bound;
-    if (cap > 2048) cap = 2048;
-    if (cap < 0) cap = 0;
-    lds += size_t(cap) * 8;
-    if (S != ell_emit(L, bt.B)) {
-        (void)hipGetLastError();
-        return hipErrorInvalidValue;
-    }
-    auto fn = cg_ell2_kernel<NT, R, S, TB, NC>;
-    allow_full_lds(reinterpret_cast<const void*>(fn));
-    launch_k(fn, dim3((L.C + NC - 1) / NC, bt.B), NT, lds, s,
-        L.m, L.C, L.base, L.at<int32_t>(ws, L.row_start), L.at<int32_t>(ws, L.row_len),
-        L.at<int32_t>(ws, L.ucnt), L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
-        L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, int(cap), st_nonconv, st_iters,
-        L.at<int32_t>(ws, L.ell_col), L.at<float>(ws, L.ell_w), bt.ws, bs, bt.u, bt.st);
-    return launch_status("solve.hip:run_ell2");
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1584,8 +1002,7 @@ template <int NT, int S, typename TB, int ND>
 __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs a,
                                                            const float* __restrict__ X,
                                                            float* __restrict__ out,
-                                                           unsigned* fsync, int32_t* st_failed,
-                                                           int poll_sleep, int pre_delay) {
+                                                           unsigned* fsync, int32_t* st_failed) {
     const int C = c.C;
     if (int(blockIdx.x) < C) {
         cg_ell_body<NT, 1, S, TB, 3>(int2{int(blockIdx.x), 0}, fsync, c.m, C, c.base,
@@ -1595,9 +1012,7 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
                                      c.ell_w, 0, 0, 0, 0);
         return;
     }
-    // ---- gradient role: one wave per row (C = 10 classes, fixed eps).  Its ~26 MB of
-    // prefetch (x_j rows) would land on top of the solves' cold prologue loads: wait first
-    for (int q = 0; q < pre_delay; ++q) __builtin_amdgcn_s_sleep(32);
+    // ---- gradient role: one wave per row (C = 10 classes, fixed eps)
     constexpr int NC = 10;
     constexpr int EB = ND <= 2 ? 16 : 8;   // grad_spmm_kernel's single-graph (WIDE) batch
     __shared__ int s_ok;
@@ -1666,13 +1081,15 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
     }
     // ---- wait for the C column solves (bounded: a lost solve surfaces as NaN + status)
     if (threadIdx.x == 0) {
-        int ok = 1;
+        // a workspace whose previous fused backward lost a solve stays poisoned (its counter may
+        // be stale) until the next forward rebuilds it: NaN again, never a stale hand-off
+        int ok = __hip_atomic_load(fsync + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
         unsigned spins = 0;
         // ~n_poll x 256 cycles between polls: 125 workgroups polling the line the solves add
         // to would otherwise queue those adds behind a storm of loads
-        while (__hip_atomic_load(fsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+        while (ok && __hip_atomic_load(fsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
                unsigned(C)) {
-            for (int q = 0; q < poll_sleep; ++q) __builtin_amdgcn_s_sleep(4);
+            for (int q = 0; q < 4; ++q) __builtin_amdgcn_s_sleep(4);
             if (++spins > (1u << 24)) {
                 ok = 0;
                 break;
@@ -1734,15 +1151,23 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
     if (tr) g_trace[18] = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) atomicMax(&g_trace[19], __builtin_amdgcn_s_memrealtime());
 #endif
-    if (threadIdx.x == 0) {   // the last gradient workgroup re-arms the counters
+    if (threadIdx.x == 0) {
+        // the last gradient workgroup re-arms the counters for a second backward over the same
+        // workspace (retain_graph) -- unless some workgroup gave up on the solves: then CG
+        // workgroups may still add to fsync[0] after a reset, so the workspace is poisoned
+        // instead (fsync[64], cleared by the next forward's row build)
+        if (!ok) {
+            __hip_atomic_fetch_or(fsync + 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (st_failed) atomicOr(st_failed, 1);
+        }
         const unsigned ng = gridDim.x - unsigned(C);
-        const unsigned old = __hip_atomic_fetch_add(fsync + 32, 1u, __ATOMIC_RELAXED,
+        const unsigned old = __hip_atomic_fetch_add(fsync + 32, 1u, __ATOMIC_ACQ_REL,
                                                     __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1u == ng) {
+        if (old + 1u == ng &&
+            __hip_atomic_load(fsync + 64, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
             __hip_atomic_store(fsync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(fsync + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (!ok && st_failed) atomicOr(st_failed, 1);
     }
 }
 
@@ -1761,14 +1186,9 @@ static hipError_t run_fused(const Layout& L, void* ws, const TB* b, const float*
     auto fn = cg_grad_fused_kernel<NT, S, TB, ND>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
     const int G = L.C + (L.n + NT / kWave - 1) / (NT / kWave);
-    int nb = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(fn), NT,
-                                                     lds) != hipSuccess)
-        nb = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipGetLastError();
-    if (int64_t(nb) * cus < G) return hipErrorNotSupported;   // not co-resident: two launches
+    // (cached per kernel and device: a HIP query per call is host time on the step's path)
+    const int nb = occupancy_blocks(reinterpret_cast<const void*>(fn), NT, lds);
+    if (int64_t(nb) * device_cus() < G) return hipErrorNotSupported;   // not co-resident: two launches
     EllCgArgs c;
     c.m = L.m;
     c.C = L.C;
@@ -1790,12 +1210,8 @@ static hipError_t run_fused(const Layout& L, void* ws, const TB* b, const float*
     c.ell_w = L.at<float>(ws, L.ell_w);
     const EdgeArgs a = make_edge_args(L, 0, ws, eps_fixed);
     prof_begin(GLL_K_BWD, s);
-    const char* ps = getenv("GLL_FUSED_SLEEP");   // diagnostic A/B of the poll interval
-    const int poll_sleep = ps ? atoi(ps) : 4;
-    const char* pd = getenv("GLL_FUSED_DELAY");   // diagnostic A/B of the prefetch delay
-    const int pre_delay = pd ? atoi(pd) : 0;
     launch_k(fn, dim3(unsigned(G)), NT, lds, s, c, a, X, gradX, L.at<unsigned>(ws, L.fsync),
-             st_failed, poll_sleep, pre_delay);
+             st_failed);
     prof_end(GLL_K_BWD, s);
     return launch_status("solve.hip:run_fused");
 }
@@ -1808,13 +1224,9 @@ hipError_t launch_cg_grad_fused(const Layout& L, void* ws, const void* gbar, int
     if (L.C != 10 || !(eps_fixed > 0.f) || !vec || m < 1 || m > 512 || L.RV != 0 ||
         ell_emit(L, 1) != 24 || L.d > 1024)
         return hipErrorNotSupported;
-    const char* fe = getenv("GLL_BWD_FUSED");   // diagnostic A/B through the torch layer
-    if ((L.flags & GLL_FLAG_BWD_UNFUSED) || (fe && fe[0] == '0') ||
-        (L.flags & (GLL_FLAG_CG_GRID | GLL_FLAG_CG_CLASSIC | GLL_FLAG_CG_PIPE | GLL_FLAG_GRAD_CHUNK)))
+    if (L.flags & (GLL_FLAG_BWD_UNFUSED | GLL_FLAG_CG_GRID | GLL_FLAG_GRAD_CHUNK))
         return hipErrorNotSupported;
     if (size_t(L.n) * L.d * 4 > (size_t(4) << 20)) return hipErrorNotSupported;   // chunked
-    if (getenv("GLL_CG_NT") || getenv("GLL_CG_MODE"))   // diagnostic CG shapes: unfused
-        return hipErrorNotSupported;
     const int nd = (L.d + 255) / 256;
 #define GLL_FUSED(NT_)                                                                       \
     {                                                                                        \
@@ -1879,16 +1291,8 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     // the Neumann form (MODE 3) wherever a thread owns one row; batched launches with two rows
     // per thread keep one SpMV per iteration (MODE 3 at 256 x 2 takes 220 VGPRs, two waves per
     // SIMD instead of three: B = 64 NS CG 21.8 -> 34.2 us; profiles/r03l_cg_neumann_ab.txt).
-    // GLL_CG_MODE = 1 / 3: A/B.
-    static const int cg_mode_env = getenv("GLL_CG_MODE") ? atoi(getenv("GLL_CG_MODE")) : 0;
 #define GLL_ELL(NT, R, S)                                                                   \
-    return (L.flags & GLL_FLAG_CG_CLASSIC)                                                  \
-               ? run_ell<NT, R, S, TB, 0>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
-                                          st_nonconv, st_iters, s)                          \
-           : (L.flags & GLL_FLAG_CG_PIPE)                                                   \
-               ? run_ell<NT, R, S, TB, 2>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
-                                          st_nonconv, st_iters, s)                          \
-           : (cg_mode_env ? cg_mode_env == 1 : (bt.B > 1 && R > 1))                          \
+    return (bt.B > 1 && R > 1)                                                              \
                ? run_ell<NT, R, S, TB, 1>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
                                           st_nonconv, st_iters, s)                          \
                : run_ell<NT, R, S, TB, 3>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
@@ -1908,35 +1312,14 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     if (m <= 128) GLL_ELL(128, 1, 24);
     if (m <= 256) GLL_ELL(256, 1, 24);
     // m <= 512: one row per thread is the lower latency for a single graph; batches run more
-    // workgroups per CU with 4 waves x 2 rows (B = 64: 44.7 -> 36.6 us per launch)
-    static const int cg_nt = getenv("GLL_CG_NT") ? atoi(getenv("GLL_CG_NT")) : 0;  // diagnostic
-    if (m <= 512 && cg_nt == 128) GLL_ELL(128, 4, 24);
-    if (m <= 512 && cg_nt == 256) GLL_ELL(256, 2, 24);
-    if (m <= 512 && bt.B == 1) GLL_ELL(512, 1, 24);
-    // batches: column pairs (cg_ell2_kernel) only on request (GLL_FLAG_CG_PAIRS; GLL_CG_NC = 2 / 4
-    // for A/B): measured slower -- B = 64 NS 21.6 -> 27.6 us per launch, B = 8 18.2 -> 25.1
-    // (profiles/r03s_cg_pairs_ab.txt): the batched solve is bound by each workgroup's iteration
-    // latency, which a second column lengthens, not by the LDS gathers it halves
-    static const int cg_nc = getenv("GLL_CG_NC") ? atoi(getenv("GLL_CG_NC")) : 1;
-    if (m <= 512 && bt.B > 1 && (cg_nc > 1 || (L.flags & GLL_FLAG_CG_PAIRS)) &&
-        cg_mode_env <= 1 && !(L.flags & (GLL_FLAG_CG_CLASSIC | GLL_FLAG_CG_PIPE))) {
-        if (cg_nt == 512)
-            return cg_nc == 4 ? run_ell2<512, 1, 24, TB, 4>(L, bt, ws, b, bs, out64, out32, rtol,
-                                                            max_iter, st_nonconv, st_iters, s)
-                              : run_ell2<512, 1, 24, TB, 2>(L, bt, ws, b, bs, out64, out32, rtol,
-                                                            max_iter, st_nonconv, st_iters, s);
-        return cg_nc == 4 ? run_ell2<256, 2, 24, TB, 4>(L, bt, ws, b, bs, out64, out32, rtol,
-                                                        max_iter, st_nonconv, st_iters, s)
-                          : run_ell2<256, 2, 24, TB, 2>(L, bt, ws, b, bs, out64, out32, rtol,
-                                                        max_iter, st_nonconv, st_iters, s);
-    }
-    // batches of at most one column workgroup per CU (B x C <= 256) run the single-graph
-    // geometry, 512 x 1 with the Neumann form: NS B = 8 18.6 -> 15.9 us per launch; with more
-    // workgroups than CUs 256 x 2 (MODE 1) keeps the lead: B = 64 21.9 against 28.2 us
-    // (profiles/r03t_cg_batched_geometry_ab.txt).  GLL_CG_BNT = 512 / 256 forces one (A/B).
-    static const int cg_bnt = getenv("GLL_CG_BNT") ? atoi(getenv("GLL_CG_BNT")) : 0;
-    if (m <= 512 && (cg_bnt == 512 || (cg_bnt == 0 && int64_t(bt.B) * L.C <= 256)))
-        GLL_ELL(512, 1, 24);
+    // workgroups per CU with 4 waves x 2 rows (B = 64: 44.7 -> 36.6 us per launch).  Batches of
+    // at most one column workgroup per CU (B x C <= 256) run the single-graph geometry, 512 x 1
+    // with the Neumann form: NS B = 8 18.6 -> 15.9 us per launch; with more workgroups than CUs
+    // 256 x 2 (MODE 1) keeps the lead: B = 64 21.9 against 28.2 us
+    // (profiles/r03t_cg_batched_geometry_ab.txt).  (Column pairs -- two right-hand sides per
+    // workgroup -- measured slower at B = 64 and 8 and were removed in round 4:
+    // profiles/r03s_cg_pairs_ab.txt.)
+    if (m <= 512 && (bt.B == 1 || int64_t(bt.B) * L.C <= 256)) GLL_ELL(512, 1, 24);
     if (m <= 512) GLL_ELL(256, 2, 24);
     if (m <= 1024) GLL_ELL(1024, 1, 16);
     if (m <= 2048) GLL_ELL(1024, 2, 16);

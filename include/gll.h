@@ -49,40 +49,43 @@ extern "C" {
                                 * the exact merge ran instead (diagnostic count) */
 #define GLL_ST_NWORDS 16
 
-/* gll_problem.flags */
+/* gll_problem.flags: code-path choices for tests and A/B runs; none changes a result beyond
+ * fp32 summation order (each is compared against the default path in tests/) */
 #define GLL_FLAG_CG_GRID 1      /* solve Luu with the whole-GPU CG even for small m */
-#define GLL_FLAG_GRAM_NARROW 2  /* Gram on 64-tiles even where 128-tiles apply (diagnostic) */
-#define GLL_FLAG_CG_CLASSIC 4   /* per-column CG: two-reduction PCG instead of the single-reduction form (diagnostic) */
-#define GLL_FLAG_CG_PERCOL 8    /* single graphs with m > 1024: per-column CG instead of the whole-GPU CG (diagnostic) */
-#define GLL_FLAG_GRAM_F32 16    /* retired in round 2 with the fp32-MFMA Gram kernels: rejected (GLL_ERR_UNSUPPORTED) */
-#define GLL_FLAG_CG_PIPE 32     /* per-column CG: pipelined PCG (one barrier per iteration) (diagnostic) */
-#define GLL_FLAG_GRAM_NOSPLIT 64 /* small single graphs: unsplit Gram tiles (one D2 plane) (diagnostic) */
+#define GLL_FLAG_CG_PERCOL 8    /* single graphs with m > 2048: per-column CG instead of the whole-GPU CG */
 #define GLL_FLAG_DIAG_GRID_OVERSUB 128 /* tests: size the whole-GPU CG at one row per workgroup,
-                                        * far past its co-resident capacity -- the cooperative
-                                        * launch must be refused */
+                                        * far past its co-resident capacity -- the launch must
+                                        * be refused */
 #define GLL_FLAG_DIAG_GRID_FAIL 256    /* tests: inject a grid-barrier failure into the
                                         * whole-GPU CG (NaN outputs + GLL_ST_SOLVE_FAILED) */
 #define GLL_FLAG_CG_ELL 512     /* per-column CG: register-ELL kernel even where the balanced
-                                 * (virtual-row) kernel would run (diagnostic) */
+                                 * (virtual-row) kernel would run */
 #define GLL_FLAG_CG_VR 1024     /* per-column CG: balanced (virtual-row) kernel wherever it can
-                                 * run (m <= 2048) (diagnostic) */
+                                 * run (m <= 2048) */
 #define GLL_FLAG_GRAD_ROWS 2048 /* feature gradient: whole-row kernel even where the
-                                 * feature-chunked one would run (diagnostic) */
+                                 * feature-chunked one would run */
 #define GLL_FLAG_GRAD_CHUNK 4096 /* feature gradient: feature-chunked kernel wherever it can
-                                  * run (d >= 128, d % 4 == 0) (diagnostic) */
-#define GLL_FLAG_GRAM_INLINE 8192 /* 128-tile Gram: split each tile's rows inline (the round-1
-                                   * kernel) instead of pre-split planes + LDS-DMA (diagnostic) */
+                                  * run (d >= 128, d % 4 == 0) */
+#define GLL_FLAG_GRAM_INLINE 8192 /* 128-tile Gram: split each tile's rows inline instead of
+                                   * pre-split planes + LDS-DMA */
 #define GLL_FLAG_BWD_UNFUSED 16384 /* single small graphs, fixed eps: adjoint CG and feature
-                                    * gradient as two launches instead of the fused one
-                                    * (diagnostic) */
-#define GLL_FLAG_CG_PAIRS 32768    /* batched per-column CG: two right-hand-side columns per
-                                    * workgroup (measured slower; diagnostic) */
-#define GLL_FLAG_D2_F32 131072     /* pre-split Gram route (batches, mid-size graphs with d > 128):
-                                    * keep the distance matrix fp32 instead of fp16 x 2^e
-                                    * (diagnostic) */
+                                    * gradient as two launches instead of the fused one */
 #define GLL_FLAG_KNN_PANEL 65536   /* single graphs: build the kNN in row panels of 1,024 rows
                                     * (an O(panel x n) distance buffer instead of n x n; automatic
                                     * past 32 GiB of n x n distances, panels of 8 GiB) */
+#define GLL_FLAG_D2_F32 131072     /* pre-split Gram route (batches): keep the distance matrix
+                                    * fp32 instead of fp16 x 2^e */
+#define GLL_FLAG_ALL (1 | 8 | 128 | 256 | 512 | 1024 | 2048 | 4096 | 8192 | 16384 | 65536 | 131072)
+/* (Retired, rejected with GLL_ERR_INVALID_ARG: 2 GRAM_NARROW, 4 CG_CLASSIC, 16 GRAM_F32,
+ * 32 CG_PIPE, 64 GRAM_NOSPLIT, 32768 CG_PAIRS -- variants that lost their A/B runs.) */
+
+/* Process-wide test knobs (gll_set_knob): each forces a code path that the automatic choice
+ * would not take on the test's shape; 0 = automatic.  None changes a result. */
+#define GLL_KNOB_VR_RV 0      /* balanced CG: virtual rows per thread (4 / 8 / 10) */
+#define GLL_KNOB_GRID_CAP 1   /* whole-GPU CG: co-resident workgroup capacity */
+#define GLL_KNOB_GRAM_TILE 2  /* pre-split Gram: 128- or 256-row tiles */
+#define GLL_KNOB_COUNT 3
+int gll_set_knob(int knob, int value);
 
 typedef struct gll_problem {
     int32_t n;        /* rows of X = base + m; labeled rows first (GLL.py:11,32) */

@@ -162,7 +162,8 @@ def test_torch_extension_module_loads():
     from graphlearninglayer_amd import GLL as GG
     ext = GG._ext()
     assert ext is not None, "_gll_torch.so missing: run __graft_entry__.build()"
-    assert hasattr(ext, "laplace_learning")
+    assert callable(ext.apply)
+    assert GG.LaplaceLearningSparseHard.apply is ext.apply   # the native function, no wrapper
 
 
 def test_k_outside_the_supported_range_raises_a_clear_error():

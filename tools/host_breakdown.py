@@ -63,13 +63,9 @@ def raw_fwd():
     lib.gll_forward(ct.byref(prob), Xd.data_ptr(), Y.data_ptr(), 0, ws.data_ptr(), Ud.data_ptr(), s)
 
 
-ext = GLL._ext()
-sink = GLL._sink(dev)[0].data_ptr()
-
-
 def ext_fwd():
     with torch.no_grad():
-        ext.laplace_learning(X, Y, 0.07, 1.0, 10, 1000, 1e-6, sink)
+        lap(X, Y, 0.07, 1.0, 10)
 
 
 def step():
