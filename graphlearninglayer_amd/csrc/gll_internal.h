@@ -30,6 +30,7 @@ constexpr int kStBump = 9;       //                        bump-region cursor
 
 // ELL slice width of the per-column CG kernels for m unlabeled rows (solve.hip dispatch);
 // row_build emits that many column-major (col, w) slots per U row, 0 when no ELL kernel runs.
+// Even: two slots per 16-B record (Layout::ell).
 inline int ell_slots(int m) {
     return m <= 512 ? 24 : (m <= 2048 ? 16 : (m <= 4096 ? 4 : 0));
 }
@@ -177,8 +178,8 @@ struct Layout {
     int64_t Etot;     // entry capacity: n Wcap slots + 2 n (K-1) bump region
     size_t status, D2, knn_idx, knn_d2, eps, rev_cnt, rev_idx, rev_d2, ovf, row_start, row_len;
     size_t tmp_col, tmp_d2, col, w, d2e, deg, ucnt, diag, rhs, P, Wadj, S, b, cgv, total;
-    int SE;           // ELL slots per U row (ell_slots)
-    size_t ell_col, ell_w;
+    int SE;           // ELL slots per U row (ell_slots; even)
+    size_t ell;       // [SE/2][m] 16-B records (col_2s, w_2s, col_2s+1, w_2s+1)
     int RV;           // balanced CG: virtual rows per thread (vr_threads), 0 = not used
     int VRM;          // balanced CG: virtual-row slots per U row (vr_max_per_row)
     size_t vr;        // [m][VRM] packed virtual rows (kVrSlot bytes each)
@@ -226,8 +227,10 @@ struct Layout {
         diag = take(size_t(m) * 4);
         rhs = take(size_t(m) * C * 4);
         SE = ell_slots(m);
-        ell_col = take(size_t(SE) * m * 4);   // [SE][m] U-block columns (U index), 0-padded
-        ell_w = take(size_t(SE) * m * 4);     // [SE][m] weights W_uj, 0-padded
+        // U-block columns (U index) and weights W_uj of each U row's first SE entries, 0-padded,
+        // two slots per 16-B record: one dwordx4 load brings two slots of a row (the CG's setup
+        // issues SE/2 loads per row instead of 2 SE)
+        ell = take(size_t(SE) * m * 8);
         RV = vr_threads(n, m, K, flags);
         VRM = RV ? vr_max_per_row(K) : 0;
         vr = take(size_t(m) * VRM * kVrSlot);

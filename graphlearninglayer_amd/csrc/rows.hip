@@ -50,8 +50,7 @@ struct RowArgs {
     float* rhs;
     float* P;
     float* Wadj;
-    int32_t* ell_col;   // [SE][m] column-major U slices for the CG (SE = 0: none)
-    float* ell_w;
+    int32_t* ell;       // [SE/2][m] x (col, w, col, w): column-major U slices for the CG
     int SE, m;
     char* vr;           // [m][VRM] packed virtual rows of the balanced CG (VRM = 0: none)
     int VRM;
@@ -81,8 +80,7 @@ struct RowArgs {
         rhs = FLAT ? gshift_flat_at(rhs, wss, g) : gshift_at(rhs, wss, g);
         P = FLAT ? gshift_flat_at(P, wss, g) : gshift_at(P, wss, g);
         Wadj = FLAT ? gshift_flat_at(Wadj, wss, g) : gshift_at(Wadj, wss, g);
-        ell_col = FLAT ? gshift_flat_at(ell_col, wss, g) : gshift_at(ell_col, wss, g);
-        ell_w = FLAT ? gshift_flat_at(ell_w, wss, g) : gshift_at(ell_w, wss, g);
+        ell = FLAT ? gshift_flat_at(ell, wss, g) : gshift_at(ell, wss, g);
         vr = FLAT ? gshift_flat_at(vr, wss, g) : gshift_at(vr, wss, g);
         fsync = FLAT ? gshift_flat_at(fsync, wss, g) : gshift_at(fsync, wss, g);
     }
@@ -221,8 +219,9 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
             const int e = nlab + (live ? lane : 0);
             const int c = live ? ocol[e] - a.base : 0;
             const float we = live ? ow[e] : 0.f;
-            a.ell_col[size_t(lane) * a.m + u] = c;
-            a.ell_w[size_t(lane) * a.m + u] = we;
+            int32_t* rec = a.ell + (size_t(lane >> 1) * a.m + u) * 4 + (lane & 1) * 2;
+            rec[0] = c;
+            rec[1] = __float_as_int(we);
         }
     }
     if (i >= a.base && a.VRM > 0) {
@@ -394,8 +393,7 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     a.rhs = L.at<float>(ws, L.rhs);
     a.P = L.at<float>(ws, L.P);
     a.Wadj = L.at<float>(ws, L.Wadj);
-    a.ell_col = L.at<int32_t>(ws, L.ell_col);
-    a.ell_w = L.at<float>(ws, L.ell_w);
+    a.ell = L.at<int32_t>(ws, L.ell);
     a.SE = ell_emit(L, bt.B);
     a.m = L.m;
     a.vr = L.at<char>(ws, L.vr);

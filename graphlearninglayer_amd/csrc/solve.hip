@@ -206,12 +206,10 @@ __device__ __forceinline__ void cg_ell_body(
     const int32_t* __restrict__ col, const float* __restrict__ wv, const float* __restrict__ diag,
     const TB* __restrict__ bsrc, double* __restrict__ out64, float* __restrict__ out32,
     float rtol, int max_iter, int mat_cap, int32_t* __restrict__ st_nonconv,
-    int32_t* __restrict__ st_iters, const int32_t* __restrict__ ell_col,
-    const float* __restrict__ ell_w, size_t wss, size_t bs,
+    int32_t* __restrict__ st_iters, const int4* __restrict__ ell, size_t wss, size_t bs,
     size_t us, size_t sts) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    ell_col = gshift_at(ell_col, wss, gxy.y);
-    ell_w = gshift_at(ell_w, wss, gxy.y);
+    ell = gshift_at(ell, wss, gxy.y);
     row_start = gshift_br_at(row_start, wss, gxy.y);   // batched launches: graph blockIdx.y
     row_len = gshift_br_at(row_len, wss, gxy.y);
     ucnt = gshift_at(ucnt, wss, gxy.y);
@@ -254,10 +252,14 @@ __device__ __forceinline__ void cg_ell_body(
         const int u = urow[q];
         const int uc = u < m ? u : 0;
         ulen[q] = ucnt[uc];
+        static_assert(S % 2 == 0, "two ELL slots per 16-B record");
 #pragma unroll
-        for (int s = 0; s < S; ++s) {   // column-major ELL slices (row_build): coalesced, padded
-            ec[q][s] = ell_col[size_t(s) * m + uc];
-            ew[q][s] = ell_w[size_t(s) * m + uc];
+        for (int s2 = 0; s2 < S / 2; ++s2) {   // column-major ELL records (row_build): coalesced
+            const int4 v = ell[size_t(s2) * m + uc];
+            ec[q][2 * s2] = v.x;
+            ew[q][2 * s2] = __int_as_float(v.y);
+            ec[q][2 * s2 + 1] = v.z;
+            ew[q][2 * s2 + 1] = __int_as_float(v.w);
         }
         dg[q] = diag[uc];
         bv[q] = to_f32(bsrc[size_t(uc) * C + c]);
@@ -533,13 +535,12 @@ __global__ __launch_bounds__(NT) void cg_ell_kernel(
     const int32_t* __restrict__ col, const float* __restrict__ wv, const float* __restrict__ diag,
     const TB* __restrict__ bsrc, double* __restrict__ out64, float* __restrict__ out32,
     float rtol, int max_iter, int mat_cap, int32_t* __restrict__ st_nonconv,
-    int32_t* __restrict__ st_iters, const int32_t* __restrict__ ell_col,
-    const float* __restrict__ ell_w, size_t wss, size_t bs,
+    int32_t* __restrict__ st_iters, const int4* __restrict__ ell, size_t wss, size_t bs,
     size_t us, size_t sts) {
     // batch_xy once: per pointer it re-reads gridDim and divides
     cg_ell_body<NT, R, S, TB, MODE>(batch_xy<true>(), nullptr, m, C, base, row_start, row_len,
                                     ucnt, col, wv, diag, bsrc, out64, out32, rtol, max_iter,
-                                    mat_cap, st_nonconv, st_iters, ell_col, ell_w, wss, bs, us,
+                                    mat_cap, st_nonconv, st_iters, ell, wss, bs, us,
                                     sts);
 }
 
@@ -963,7 +964,7 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
         L.m, L.C, L.base, L.at<int32_t>(ws, L.row_start), L.at<int32_t>(ws, L.row_len),
         L.at<int32_t>(ws, L.ucnt), L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
         L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, int(cap), st_nonconv, st_iters,
-        L.at<int32_t>(ws, L.ell_col), L.at<float>(ws, L.ell_w), bt.ws, bs, bt.u, bt.st);
+        L.at<int4>(ws, L.ell), bt.ws, bs, bt.u, bt.st);
     return launch_status("solve.hip:run_ell");
 }
 
@@ -994,8 +995,7 @@ struct EllCgArgs {
     int max_iter, mat_cap;
     int32_t* st_nonconv;
     int32_t* st_iters;
-    const int32_t* ell_col;
-    const float* ell_w;
+    const int4* ell;
 };
 
 template <int NT, int S, typename TB, int ND>
@@ -1008,8 +1008,8 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
         cg_ell_body<NT, 1, S, TB, 3>(int2{int(blockIdx.x), 0}, fsync, c.m, C, c.base,
                                      c.row_start, c.row_len, c.ucnt, c.col, c.wv, c.diag,
                                      static_cast<const TB*>(c.b), nullptr, c.out32, c.rtol,
-                                     c.max_iter, c.mat_cap, c.st_nonconv, c.st_iters, c.ell_col,
-                                     c.ell_w, 0, 0, 0, 0);
+                                     c.max_iter, c.mat_cap, c.st_nonconv, c.st_iters, c.ell,
+                                     0, 0, 0, 0);
         return;
     }
     // ---- gradient role: one wave per row (C = 10 classes, fixed eps)
@@ -1206,8 +1206,7 @@ static hipError_t run_fused(const Layout& L, void* ws, const TB* b, const float*
     c.mat_cap = int(cap);
     c.st_nonconv = st_nonconv;
     c.st_iters = st_iters;
-    c.ell_col = L.at<int32_t>(ws, L.ell_col);
-    c.ell_w = L.at<float>(ws, L.ell_w);
+    c.ell = L.at<int4>(ws, L.ell);
     const EdgeArgs a = make_edge_args(L, 0, ws, eps_fixed);
     prof_begin(GLL_K_BWD, s);
     launch_k(fn, dim3(unsigned(G)), NT, lds, s, c, a, X, gradX, L.at<unsigned>(ws, L.fsync),
