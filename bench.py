@@ -586,6 +586,47 @@ def main():
     if not a.no_profile:
         c_abi = c_abi_measure(X, Y, tau, eps, k, gbar, a.steps, a.warmup)
 
+    # the adversarial scripts' inline-copy call (train_and_adversarial.py:721,745;
+    # adversarial.py:534): lap(features, one_hot(labels)[:k]) -- int64 labels, tau = 0, eps =
+    # 'auto' -- on the same graph, through apply + autograd.grad (labelled extra, not `value`)
+    auto_extra = None
+    if a.config == "ns" and not a.no_profile and world == 1:
+        Yi = Y.to(torch.int64)
+        per_k = {}
+
+        def step_auto_k():
+            U_ = lap(X, Yi, 0, "auto", k)
+            return torch.autograd.grad(U_, X, gbar)
+
+        for fn_ in (step_auto_k,):
+            for _ in range(a.warmup):
+                fn_()
+            torch.cuda.synchronize()
+            for q in range(_lib.K_COUNT):
+                _lib.prof_enable(q, 1)
+            for _ in range(10):
+                fn_()
+            torch.cuda.synchronize()
+            for q in range(_lib.K_COUNT):
+                ms_, cnt_ = _lib.prof_read(q)
+                _lib.prof_enable(q, 0)
+                if cnt_:
+                    per_k[names[q]] = {"us_per_launch": round(1e3 * ms_ / cnt_, 3),
+                                       "launches_per_step": cnt_ / 10}
+            torch.cuda.synchronize()
+            t0_ = time.perf_counter()
+            for _ in range(a.steps):
+                fn_()
+            torch.cuda.synchronize()
+            el_ = time.perf_counter() - t0_
+        GLL.check_status()
+        auto_extra = {"call": f"lap(X, one_hot int64, tau=0, epsilon='auto', k={k})",
+                      "reference": "train_and_adversarial.py:721,745; adversarial.py:534",
+                      "value": round(a.steps / el_, 3), "unit": "calls/s",
+                      "ms_per_step": round(1e3 * el_ / a.steps, 4), "kernels": per_k,
+                      "note": "same NS graph inputs as the headline, the inline-copy callers' "
+                              "epsilon / tau / label dtype (k kept at the workload's 10)"}
+
     batched = None
     if a.batch > 0 and roofline is not None:
         batched = batched_measure(c, eps, tau, k, a.batch, gstats, dev, rank)
@@ -596,9 +637,13 @@ def main():
 
     if rank == 0:
         calls = world * a.steps
+        # every GLL_* variable of this process: the product library reads only GLL_DEBUG (it
+        # prints launch errors); GLL_LIB_PATH loads another build (A/B), so no value is reported
+        gll_env = {kk: vv for kk, vv in sorted(os.environ.items()) if kk.startswith("GLL_")}
+        foreign = sorted(kk for kk in gll_env if kk not in ("GLL_DEBUG",))
         out = {
             "metric": METRIC,
-            "value": round(calls / elapsed, 3),
+            "value": None if foreign else round(calls / elapsed, 3),
             "unit": "calls/s",
             "n_gpus": world,
             "steps": a.steps,
@@ -622,7 +667,12 @@ def main():
             "kernels": per_kernel,
             "c_abi": c_abi,
             "batched": batched,
+            "auto_eps_extra": auto_extra,
+            "gll_env": gll_env,
         }
+        if foreign:
+            out["invalid"] = (f"GLL_* variables that change what runs are set ({', '.join(foreign)}): "
+                              "not a measurement of the product library")
         if roofline is not None:
             step_s = elapsed / a.steps
             out["call_roofline"] = {

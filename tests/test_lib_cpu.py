@@ -178,3 +178,16 @@ def test_k_outside_the_supported_range_raises_a_clear_error():
             GLL.LaplaceLearningSparseHard.apply(X, Y, 0.0, 1.0, k)
     with pytest.raises(ValueError, match="2 <= min"):
         GLL.device_graph(X, 64)
+
+
+def test_product_library_reads_no_switch_but_debug():
+    """The product libgll.so reads no environment switch that skips work or changes a path:
+    the only GLL_* name in it is GLL_DEBUG (prints launch errors).  Code paths for tests are
+    gll_problem.flags and gll_set_knob (include/gll.h), which tests compare against the
+    default path; bench.py refuses a value when another GLL_* variable is set."""
+    import subprocess
+    from graphlearninglayer_amd import _lib
+    out = subprocess.run(["strings", "-a", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    names = sorted(set(re.findall(r"\bGLL_[A-Z0-9_]+", out)))
+    assert names == ["GLL_DEBUG"], names
