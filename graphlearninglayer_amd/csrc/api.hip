@@ -214,6 +214,7 @@ static int build_graph(const gll_problem* p, const Layout& L, const Batch& bt, c
         }
     } else {
         if (launch_gram(L, bt, ws, X, vec, s) != hipSuccess) return GLL_ERR_HIP;
+        if (locality_order(L, bt) && launch_order(L, ws, s) != hipSuccess) return GLL_ERR_HIP;
         if (launch_select(L, bt, ws, X, p->eps, auto_eps, vec, public_status(p, L, ws), s) !=
             hipSuccess)
             return GLL_ERR_HIP;

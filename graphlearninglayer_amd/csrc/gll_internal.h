@@ -27,6 +27,9 @@ constexpr int kMaxKm1 = 56;      // K - 1 <= 56: the kNN rescan keeps >= 8 lanes
 // ---------------------------------------------------------------------------------------
 constexpr int kStOvfCount = 8;   // internal status words: overflow-list length
 constexpr int kStBump = 9;       //                        bump-region cursor
+constexpr int kPiv = 64;         // pivot rows of the locality order (order_pid_kernel)
+constexpr int kStPiv = GLL_ST_NWORDS;   // [kPiv] rows per pivot, then [kPiv] scatter cursors
+constexpr int kStWords = GLL_ST_NWORDS + 2 * kPiv;   // words the Gram kernels zero per call
 
 // ELL slice width of the per-column CG kernels for m unlabeled rows (solve.hip dispatch);
 // row_build emits that many column-major (col, w) slots per U row, 0 when no ELL kernel runs.
@@ -188,6 +191,7 @@ struct Layout {
     size_t fsync;     // fused backward: [0] solved columns, [32] finished gradient blocks,
                       // [64] poison (a lost solve: the counters may be stale)
     size_t d2s;       // float: the fp16 D2 scale of the pre-split GEMM (knn.hip tile_d2_scale)
+    size_t pid, perm; // locality order (order_rows): nearest pivot of each row, the row order
 
     explicit Layout(const gll_problem& p) {
         n = p.n; d = p.d; base = p.base; C = p.C;
@@ -206,7 +210,7 @@ struct Layout {
             off += (bytes + 255) & ~size_t(255);
             return at;
         };
-        status = take(GLL_ST_NWORDS * 4);
+        status = take(size_t(kStWords) * 4);
         D2 = take(size_t(KS) * PR * ldD * 4);  // KS partial planes (or one panel)
         knn_idx = take(size_t(n) * K * 4);
         knn_d2 = take(size_t(n) * K * 4);
@@ -240,6 +244,8 @@ struct Layout {
         xnrm = take(size_t(n) * 4);
         fsync = take(384);   // three words on their own 128-B lines, zeroed by row_build
         d2s = take(256);     // fp16 D2 scale of the pre-split Gram (knn.hip tile_d2_scale)
+        pid = take(size_t(n) * 4);
+        perm = take(size_t(n) * 4);
         P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)
         Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
         S = take(size_t(Etot) * 4);        // per-edge coefficient (auto eps / chunked gradient)
@@ -554,6 +560,17 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
                          hipStream_t s, int r0 = 0, int rows = -1);
 hipError_t launch_gram_panel(const Layout& L, void* ws, const float* X, bool vec, int r0, int rows,
                              hipStream_t s);
+// Locality order of the rows of one large graph (knn.hip order_rows): rows grouped by their
+// nearest of kPiv pivot rows under the Gram distances, so each XCD's share of the select and of
+// the chunked gradient is a run of rows whose neighbours mostly lie in the same run -- the X rows
+// those kernels gather then stay in that XCD's 4 MB L2 instead of streaming from the MALL.  Speed
+// only: every row's result is independent of the order.  Single graphs whose X exceeds an XCD's
+// L2 (n d 4 B > 4 MB), with the whole n x n distance matrix (no row panels).
+inline bool locality_order(const Layout& L, const Batch& bt) {
+    return bt.B == 1 && L.PR == L.n && L.n >= 16 * kPiv &&
+           size_t(L.n) * L.d * 4 > (size_t(4) << 20) && !(L.flags & GLL_FLAG_ROW_ORDER_OFF);
+}
+hipError_t launch_order(const Layout& L, void* ws, hipStream_t s);
 hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,
                            int y_dtype, float tau, float eps_fixed, hipStream_t s);
 // b: right-hand sides of graph 0, `b_stride` bytes apart (the workspace rhs or gbar)

@@ -181,7 +181,8 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
 template <int COEF, int LPR>
 __global__ __launch_bounds__(256) void grad_chunk_kernel(EdgeArgs a, const float* __restrict__ X,
                                                          float* __restrict__ out, int nch,
-                                                         size_t xs, size_t gxs) {
+                                                         size_t xs, size_t gxs,
+                                                         const int32_t* __restrict__ perm) {
     GLL_TRACE_SCOPE(1);
     a.to_graph();
     X = gshift(X, xs);
@@ -192,8 +193,11 @@ __global__ __launch_bounds__(256) void grad_chunk_kernel(EdgeArgs a, const float
     const int gl = lane % LPR;                // lane inside the row's group
     const int blk = bx();
     const int chunk = blk % nch;
-    const int i = (blk / nch) * (4 * RPW) + (threadIdx.x >> 6) * RPW + lane / LPR;
-    const bool live = i < a.n;
+    // row position in time order: the locality order of a large graph (gll_internal.h
+    // locality_order) when given, so a chunk's XCD gathers the neighbour rows of nearby rows
+    const int pos = (blk / nch) * (4 * RPW) + (threadIdx.x >> 6) * RPW + lane / LPR;
+    const bool live = pos < a.n;
+    const int i = live ? (perm ? perm[pos] : pos) : pos;
     const int ic = live ? i : 0;
     const int d = a.d;
     const int k = chunk * 4 * LPR + 4 * gl;   // this lane's 4 features
@@ -259,18 +263,18 @@ static bool grad_use_chunks(const Layout& L, const Batch& bt, bool vec) {
 // LPR = the power of two nearest d / 32 in [16, 64], NCH = ceil(d / (4 LPR)) chunks.
 template <int COEF>
 static void grad_chunked(const EdgeArgs& a, const Batch& bt, const float* X, float* out,
-                         hipStream_t s) {
+                         const int32_t* perm, hipStream_t s) {
     int lpr = 16;
     while (lpr < 64 && 4 * lpr * 8 < a.d) lpr *= 2;
     const int nch = (a.d + 4 * lpr - 1) / (4 * lpr);
     const int rows_per_block = 4 * (kWave / lpr);
     dim3 grid(unsigned(nch * ((a.n + rows_per_block - 1) / rows_per_block)), bt.B);
     if (lpr == 16)
-        launch_k(grad_chunk_kernel<COEF, 16>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx);
+        launch_k(grad_chunk_kernel<COEF, 16>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx, perm);
     else if (lpr == 32)
-        launch_k(grad_chunk_kernel<COEF, 32>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx);
+        launch_k(grad_chunk_kernel<COEF, 32>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx, perm);
     else
-        launch_k(grad_chunk_kernel<COEF, 64>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx);
+        launch_k(grad_chunk_kernel<COEF, 64>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx, perm);
 }
 
 template <bool AUTO, bool VEC, int CV>
@@ -324,8 +328,9 @@ hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, cons
     }
     prof_begin(GLL_K_GRAD, s);
     if (chunk) {
-        if (auto_eps) grad_chunked<1>(a, bt, X, gradX, s);
-        else grad_chunked<2>(a, bt, X, gradX, s);
+        const int32_t* perm = locality_order(L, bt) ? L.at<int32_t>(ws, L.perm) : nullptr;
+        if (auto_eps) grad_chunked<1>(a, bt, X, gradX, perm, s);
+        else grad_chunked<2>(a, bt, X, gradX, perm, s);
         e = launch_status("grad.hip:grad_chunked");
     } else if (auto_eps) {
         e = vec ? grad_nd<true, true, 0>(a, bt, X, gradX, s)

@@ -220,7 +220,7 @@ __global__ __launch_bounds__(1024) void gram_bf3_kernel(const float* __restrict_
     const int bj = bi + rem;
     {   // per-call reset of the counters the select kernel accumulates into
         const int g = bx() * 1024 + tid;
-        if (g < GLL_ST_NWORDS) status[g] = 0;
+        if (g < kStWords) status[g] = 0;
         for (int q = g; q < n; q += gridDim.x * 1024) rev_cnt[q] = 0;
     }
     const int fo = 4 * lane;   // this lane's 4 features inside a phase
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(1024) void gram_bf3s_kernel(const float* __restrict
     }
     {   // per-call reset of the counters the select kernel accumulates into
         const int g = bx() * 1024 + tid;
-        if (g < GLL_ST_NWORDS) status[g] = 0;
+        if (g < kStWords) status[g] = 0;
         for (int q = g; q < n; q += gridDim.x * 1024) rev_cnt[q] = 0;
     }
     const int fo = 4 * lane;
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(1024) void gram_bf3w_kernel(const float* __restrict
     }
     if (r0 == 0) {   // per-call reset of the counters the select kernel accumulates into
         const int g = bx() * 1024 + tid;
-        if (g < GLL_ST_NWORDS) status[g] = 0;
+        if (g < kStWords) status[g] = 0;
         for (int q = g; q < n; q += gridDim.x * 1024) rev_cnt[q] = 0;
     }
     const int fo = 4 * (tid & 31);       // this thread's 4 features inside a phase
@@ -668,7 +668,7 @@ __global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict
     rev_cnt = gshift_br(rev_cnt, wss);
     {   // per-call reset of the counters the select kernel accumulates into
         const int g = bx() * 256 + threadIdx.x;
-        if (g < GLL_ST_NWORDS) status[g] = 0;
+        if (g < kStWords) status[g] = 0;
         for (int q = g; q < n; q += gridDim.x * 256) rev_cnt[q] = 0;
     }
     const int lane = lane_id();
@@ -1493,7 +1493,7 @@ void knn_select_kernel(
     float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ rev_cnt,
     int32_t* __restrict__ rev_idx, float* __restrict__ rev_d2, int32_t* __restrict__ ovf,
     int32_t* __restrict__ status, int32_t* __restrict__ status_pub, size_t xs, size_t wss,
-    size_t sts, int r0, int r1, const float* __restrict__ d2s) {
+    size_t sts, int r0, int r1, const float* __restrict__ d2s, const int32_t* __restrict__ perm) {
     GLL_TRACE_SCOPE(1);
     GLL_TRACE_PT(20);
     const int2 gxy = batch_xy<R>();   // once (per pointer it re-reads gridDim and divides)
@@ -1515,8 +1515,18 @@ void knn_select_kernel(
     __shared__ float s_xi[XL ? 4 : 1][XL ? 256 * XQ : 1];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
-    const int i = r0 + gxy.x * 4 + wv;   // rows r0 .. r1 - 1: all, or a panel (D2 row i - r0)
-    if (i >= r1) return;  // whole wave
+    // rows r0 .. r1 - 1: all, or a panel (D2 row i - r0); with a locality order (one large graph,
+    // no panels) block b takes positions of the order dealt XCD-contiguously (xcd_tile): each
+    // XCD works through a run of rows whose neighbours mostly lie in that same run
+    int i;
+    if (perm) {
+        const int sl = xcd_tile(int(blockIdx.x), int(gridDim.x)) * 4 + wv;
+        if (sl >= r1) return;  // whole wave
+        i = perm[sl];
+    } else {
+        i = r0 + gxy.x * 4 + wv;
+        if (i >= r1) return;  // whole wave
+    }
     // XL: x_i is staged once in LDS (its loads ride under the D2 scan's), so the exact
     // distances hold only the candidates' rows in registers (occupancy) and do not re-load x_i
     // per sweep.  Features past d are zero (masked at use anyway).
@@ -1992,6 +2002,86 @@ static bool d2_half(const Layout& L, const Batch& bt) {
     return !(L.flags & GLL_FLAG_D2_F32) && bt.B > 1 && presplit_route(L, bt);
 }
 
+// --------------------------------------------------------------------------------------
+// Locality order of the rows of one large graph (gll_internal.h locality_order).  Pivot j is
+// row (j * 2654435761 + 12345) mod n -- a hash, so periodic row layouts (labels i % 10 in the
+// callers' minibatches) do not alias -- and row i joins the pivot nearest to it under the Gram
+// D2, read as the pivots' D2 rows (D2 is symmetric; coalesced across i).  Ties go to the lower
+// pivot; a NaN distance never wins.  Speed only: no row's result depends on the order.
+// --------------------------------------------------------------------------------------
+__device__ __forceinline__ int pivot_row(int j, int n) {
+    return int((uint32_t(j) * 2654435761u + 12345u) % uint32_t(n));
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void order_pid_kernel(const float* __restrict__ D2, int ld,
+                                                        size_t plane, int n,
+                                                        int32_t* __restrict__ pid,
+                                                        int32_t* __restrict__ status) {
+    const int i = int(blockIdx.x) * 256 + int(threadIdx.x);
+    if (i >= n) return;
+    float v[kPiv];
+#pragma unroll
+    for (int j = 0; j < kPiv; ++j) {   // every load issued before any is compared
+        const size_t o = size_t(pivot_row(j, n)) * ld + i;
+        v[j] = D2[o];
+#pragma unroll
+        for (int p = 1; p < NP; ++p) v[j] += D2[p * plane + o];
+    }
+    float best = __builtin_inff();
+    int bp = 0;
+#pragma unroll
+    for (int j = 0; j < kPiv; ++j)
+        if (v[j] < best) {
+            best = v[j];
+            bp = j;
+        }
+    pid[i] = bp;
+    atomicAdd(&status[kStPiv + bp], 1);
+}
+
+// One workgroup: the pivots' row counts -> offsets (wave 0's scan), then every row to its
+// pivot's range (LDS cursors; the order inside a range is arbitrary -- speed only).
+__global__ __launch_bounds__(1024) void order_perm_kernel(int n, const int32_t* __restrict__ pid,
+                                                          const int32_t* __restrict__ status,
+                                                          int32_t* __restrict__ perm) {
+    static_assert(kPiv == kWave, "one wave scans the pivot counts");
+    __shared__ int base[kPiv];
+    __shared__ int cur[kPiv];
+    const int tid = threadIdx.x;
+    if (tid < kWave) {
+        const int c = status[kStPiv + tid];
+        int incl = c;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const int t = __shfl_up(incl, off);
+            if (tid >= off) incl += t;
+        }
+        base[tid] = incl - c;
+        cur[tid] = 0;
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        const int p = pid[i];
+        perm[base[p] + atomicAdd(&cur[p], 1)] = i;
+    }
+}
+
+hipError_t launch_order(const Layout& L, void* ws, hipStream_t s) {
+    const float* D2 = L.at<float>(ws, L.D2);
+    int32_t* st = L.at<int32_t>(ws, L.status);
+    int32_t* pid = L.at<int32_t>(ws, L.pid);
+    const size_t plane = size_t(L.n) * L.ldD;
+    const dim3 grid(unsigned((L.n + 255) / 256));
+    if (gram_planes(L, 1) == 2)
+        launch_k(order_pid_kernel<2>, grid, 256, 0, s, D2, L.ldD, plane, L.n, pid, st);
+    else
+        launch_k(order_pid_kernel<1>, grid, 256, 0, s, D2, L.ldD, plane, L.n, pid, st);
+    launch_k(order_perm_kernel, dim3(1), 1024, 0, s, L.n, static_cast<const int32_t*>(pid),
+             static_cast<const int32_t*>(st), L.at<int32_t>(ws, L.perm));
+    return launch_status("knn.hip:launch_order");
+}
+
 hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* X, bool vec,
                        hipStream_t s) {
     float* D2 = L.at<float>(ws, L.D2);
@@ -2109,6 +2199,8 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     dim3 grid((rows + 3) / 4, bt.B);
     const bool h16 = planes == 1 && d2_half(L, bt);   // the Gram stored D2 as fp16 x s
     const float* d2s = L.at<float>(ws, L.d2s);
+    const int32_t* perm = (locality_order(L, bt) && r0 == 0 && rows == n)
+                              ? L.at<int32_t>(ws, L.perm) : nullptr;
     prof_begin(GLL_K_SELECT, s);
 // Batched launches (PG = 1) stage x_i in LDS (XQ quarters of 256 features, d <= 1024) and run at
 // 6 waves per SIMD: measured at B = 64 NS, select 259 -> 214 us (XQ = 2, NU = 8; the NU = 16
@@ -2126,7 +2218,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
         L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps),       \
         L.at<int32_t>(ws, L.rev_cnt), L.at<int32_t>(ws, L.rev_idx), L.at<float>(ws, L.rev_d2), \
         L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), status_pub, bt.x, bt.ws, bt.st,       \
-        r0, r0 + rows, d2s)
+        r0, r0 + rows, d2s, perm)
 #define GLL_SEL5(KCV, V, NPV, NUS, NUB, XQV, CHV)                                              \
     do {                                                                                       \
         if (h16) GLL_SEL6(KCV, V, NPV, NUS, NUB, XQV, CHV, (NPV == 1));                        \

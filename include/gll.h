@@ -75,7 +75,11 @@ extern "C" {
                                     * past 32 GiB of n x n distances, panels of 8 GiB) */
 #define GLL_FLAG_D2_F32 131072     /* pre-split Gram route (batches): keep the distance matrix
                                     * fp32 instead of fp16 x 2^e */
-#define GLL_FLAG_ALL (1 | 8 | 128 | 256 | 512 | 1024 | 2048 | 4096 | 8192 | 16384 | 65536 | 131072)
+#define GLL_FLAG_ROW_ORDER_OFF 262144 /* large single graphs: process the kNN select and the
+                                       * chunked gradient in row-index order instead of the
+                                       * pivot-grouped locality order (A/B; results identical) */
+#define GLL_FLAG_ALL (1 | 8 | 128 | 256 | 512 | 1024 | 2048 | 4096 | 8192 | 16384 | 65536 | \
+                      131072 | 262144)
 /* (Retired, rejected with GLL_ERR_INVALID_ARG: 2 GRAM_NARROW, 4 CG_CLASSIC, 16 GRAM_F32,
  * 32 CG_PIPE, 64 GRAM_NOSPLIT, 32768 CG_PAIRS -- variants that lost their A/B runs.) */
 

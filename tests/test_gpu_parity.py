@@ -1041,3 +1041,21 @@ def test_gram_256_tiles_match_128_tiles(cfg, B, n_extra, d, monkeypatch):
     _lib.set_knob(_lib.KNOB_GRAM_TILE, 0)
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("eps", [1.0, "auto"])
+def test_locality_order_changes_no_result(eps):
+    """Large single graphs process the kNN select and the chunked gradient in a pivot-grouped
+    row order (gll_internal.h locality_order: speed only).  At the stress shape (X 32 MB, past an
+    XCD's L2) U and grad_X are bitwise those of row-index order (GLL_FLAG_ROW_ORDER_OFF), and the
+    kNN lists, eps and CSR too (GLL.py:183,205)."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth
+    c = CONFIGS["stress"]
+    X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=5)
+    Y = one_hot(lab[: c["base"]])
+    g = seeded_gbar(c["batch"], 10, 6)
+    U0, g0 = _fwd_bwd_c_abi(X, Y, c["k"], 0.07, eps, g)
+    U1, g1 = _fwd_bwd_c_abi(X, Y, c["k"], 0.07, eps, g, flags=_lib.FLAG_ROW_ORDER_OFF)
+    np.testing.assert_array_equal(U0, U1)
+    np.testing.assert_array_equal(g0, g1)
