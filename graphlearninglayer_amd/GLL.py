@@ -78,8 +78,12 @@ def _warn_from(st):
     """The warnings / error of one copy of the status words (as _gll_torch raises them), for
     callers of the C ABI that read the words themselves."""
     if st[_lib.ST_SOLVE_FAILED]:
-        raise RuntimeError("GLL: a whole-GPU CG solve lost a grid barrier (a workgroup never "
-                           "arrived); its outputs were written as NaN")
+        raise RuntimeError("GLL: the fused backward's gradient gave up waiting for the adjoint "
+                           "solves; its grad_X was written as NaN")
+    if st[_lib.ST_GRID_RESCUED]:
+        warnings.warn(f"GLL: {st[_lib.ST_GRID_RESCUED]} whole-GPU CG solve(s) lost their grid "
+                      "barrier (other kernels held the CUs) and were solved by one workgroup "
+                      "instead: correct, slower", RuntimeWarning)
     if st[_lib.ST_TINY_EPS]:
         warnings.warn("Epsilon in KNN is very close to zero.", UserWarning)  # GLL.py:240-241
     if st[_lib.ST_FWD_NONCONV]:

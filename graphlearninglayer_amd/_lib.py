@@ -32,7 +32,8 @@ FLAG_ROW_ORDER_OFF = 262144   # large single graphs: row-index order instead of 
 KNOB_VR_RV, KNOB_GRID_CAP, KNOB_GRAM_TILE = 0, 1, 2
 ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
 ST_KNN_RESCAN = 5   # kNN rows re-ranked over every column under the Gram error bound
-ST_SOLVE_FAILED = 6   # a whole-GPU CG lost a grid barrier: outputs NaN, raised as an error
+ST_SOLVE_FAILED = 6   # the fused backward gave up on its adjoint solves: grad NaN, raised
+ST_GRID_RESCUED = 10  # whole-GPU CG solves rescued by one workgroup after a lost grid barrier
 ST_KNN_MERGE = 7   # kNN rows that took the exact candidate merge (diagnostic)
 ST_NWORDS = 16
 K_GRAM, K_SELECT, K_FINALIZE, K_CG, K_EDGE, K_GRAD = range(6)

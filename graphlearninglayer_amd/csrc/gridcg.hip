@@ -86,6 +86,8 @@ struct GridCgArgs {
     int32_t* st_iters;
     int32_t* st_nonconv;
     int32_t* st_failed;      // public GLL_ST_SOLVE_FAILED word
+    int32_t* st_rescued;     // public GLL_ST_GRID_RESCUED word
+    float* rescue;           // 5 m floats: the rescue solve's vectors
 };
 
 // Hand-off discipline (cdna_hip_programming.md Guideline 16 R1; MI355X_MICROARCH.md
@@ -183,6 +185,125 @@ __device__ __forceinline__ void grid_totals(const float* part, int G, int slot, 
 __device__ __forceinline__ float rhs_at(const void* b, int dt, size_t i) {
     return dt == GLL_DT_F64 ? float(static_cast<const double*>(b)[i])
                             : static_cast<const float*>(b)[i];
+}
+
+// ---------------------------------------------------------------------------------------
+// Rescue of a lost grid barrier.  The grid kernels need every workgroup resident at once; an
+// ordinary launch does not promise that when other kernels hold CUs (a caller's side stream,
+// an RCCL kernel that waits on a peer).  A barrier that times out (~1 s) no longer ends the
+// solve with NaN: the first workgroup to see the failure claims the rescue word and solves
+// every column alone -- per-column Jacobi PCG, the same iteration and stopping rule, vectors
+// in the workspace (write-through sc1 accesses; one workgroup, so its barriers suffice) --
+// while every other workgroup leaves without writing.  It depends on no other workgroup, so it
+// always completes; the solve is slower (one CU) and GLL_ST_GRID_RESCUED counts it.
+// ---------------------------------------------------------------------------------------
+template <int NT>
+__device__ float rescue_sum(float v, float* red) {
+    v = wave_sum_dpp(v);
+    __syncthreads();   // red is free (the previous sum was read)
+    if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NT / kWave; ++w) t += red[w];
+    return t;
+}
+
+template <class Mat, int NT>
+__device__ void rescue_solve(const Mat& A, int m, int C, const void* b, int b_dtype, float rtol,
+                             float atol, int max_iter, double* out64, float* out32,
+                             float* scr /* 5 m floats */, int32_t* st_iters,
+                             int32_t* st_nonconv, int32_t* st_rescued) {
+    __shared__ float red[NT / kWave];
+    float *X_ = scr, *R_ = scr + m, *P_ = scr + 2 * size_t(m), *Q_ = scr + 3 * size_t(m),
+          *M_ = scr + 4 * size_t(m);
+    int it_max = 0, nonconv = 0;
+    for (int c = 0; c < C; ++c) {
+        float rz = 0.f, bb = 0.f;
+        for (int u = threadIdx.x; u < m; u += NT) {
+            const float dg = A.diagonal(u);
+            const float mi = dg > 0.f ? 1.f / dg : 0.f;
+            const float bu = mi > 0.f ? rhs_at(b, b_dtype, size_t(u) * C + c) : 0.f;
+            st_shared(X_ + u, 0.f);
+            st_shared(R_ + u, bu);
+            st_shared(M_ + u, mi);
+            st_shared(P_ + u, mi * bu);
+            rz += bu * mi * bu;
+            bb += bu * bu;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        rz = rescue_sum<NT>(rz, red);
+        bb = rescue_sum<NT>(bb, red);
+        const float t = fmaxf(atol, rtol * sqrtf(bb));
+        const float tol2 = t * t;
+        bool conv = !(bb > tol2);
+        int it = 0;
+        while (!conv && it < max_iter) {
+            ++it;
+            float pq = 0.f;
+            for (int u = threadIdx.x; u < m; u += NT) {
+                float acc = Mat::kSeparateDiag ? A.diagonal(u) * ld_shared(P_ + u) : 0.f;
+                for (int e = A.begin(u); e < A.end(u); ++e)
+                    acc += A.value(e) * ld_shared(P_ + A.column(e));
+                st_shared(Q_ + u, acc);
+                pq += ld_shared(P_ + u) * acc;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            pq = rescue_sum<NT>(pq, red);
+            if (!(pq > 0.f)) break;   // breakdown or NaN: non-converged
+            const float alpha = rz / pq;
+            float rr = 0.f, rzn = 0.f;
+            for (int u = threadIdx.x; u < m; u += NT) {
+                st_shared(X_ + u, ld_shared(X_ + u) + alpha * ld_shared(P_ + u));
+                const float ru = ld_shared(R_ + u) - alpha * ld_shared(Q_ + u);
+                st_shared(R_ + u, ru);
+                rr += ru * ru;
+                rzn += ru * ld_shared(M_ + u) * ru;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            rr = rescue_sum<NT>(rr, red);
+            rzn = rescue_sum<NT>(rzn, red);
+            if (rr <= tol2) {
+                conv = true;
+                break;
+            }
+            const float beta = rzn / rz;
+            rz = rzn;
+            for (int u = threadIdx.x; u < m; u += NT)
+                st_shared(P_ + u, ld_shared(M_ + u) * ld_shared(R_ + u) + beta * ld_shared(P_ + u));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        for (int u = threadIdx.x; u < m; u += NT) {
+            const float xv = ld_shared(X_ + u);
+            if (out64) out64[size_t(u) * C + c] = double(xv);
+            if (out32) out32[size_t(u) * C + c] = xv;
+        }
+        it_max = it > it_max ? it : it_max;
+        nonconv += conv ? 0 : 1;
+        __syncthreads();   // the next column reuses the vectors
+    }
+    if (threadIdx.x == 0) {
+        if (st_iters) atomicMax(st_iters, it_max);
+        if (st_nonconv && nonconv) atomicAdd(st_nonconv, nonconv);
+        if (st_rescued) atomicAdd(st_rescued, 1);
+    }
+}
+
+// After a grid kernel's loop: true when this workgroup wrote nothing because a barrier failed
+// (it rescued the solve, or another workgroup does).
+template <class Mat, int NT, class Args>
+__device__ bool rescued(bool ok, unsigned* rescue_word, const Mat& A, const Args& a,
+                        float* scr, int* s_flag) {
+    if (ok) return false;
+    if (threadIdx.x == 0)
+        *s_flag = __hip_atomic_fetch_add(rescue_word, 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) == 0u;
+    __syncthreads();
+    if (*s_flag)
+        rescue_solve<Mat, NT>(A, a.m, a.C, a.b, a.b_dtype, a.rtol, a.atol, a.max_iter, a.out64,
+                              a.out32, scr, a.st_iters, a.st_nonconv, a.st_rescued);
+    return true;
 }
 
 __device__ __forceinline__ f32x4 quad_of(const float* s, int q) {
@@ -394,11 +515,9 @@ __global__ __launch_bounds__(kGT) void cg_grid_classic_kernel(Mat A, GridCgArgs 
         if (it == 1) GLL_TRACE_PT(6);
     }
     GLL_TRACE_PT(1);
-    // a failed grid barrier (a workgroup never arrived within ~1 s) leaves x partial: the
-    // outputs become NaN and GLL_ST_SOLVE_FAILED is raised, so the failure surfaces in the
-    // caller's loss at once and as an exception at the next status check -- never as a
-    // plausible-looking U
-    const float nanf_ = __builtin_nanf("");
+    // a failed grid barrier (a workgroup never arrived within ~1 s): one workgroup solves the
+    // system alone (rescue_solve), the others write nothing
+    if (rescued<Mat, kGT>(ok, a.sync + 2, A, a, a.rescue, &s_ok)) return;
 #pragma unroll
     for (int k = 0; k < RPG; ++k) {
         const int u = r0 + grp + k * NG;
@@ -408,9 +527,8 @@ __global__ __launch_bounds__(kGT) void cg_grid_classic_kernel(Mat A, GridCgArgs 
             const int c = 4 * li + t;
             if (c < C) {
                 const size_t i = size_t(u) * C + c;
-                const float xv = ok ? x[k][t] : nanf_;
-                if (a.out64) a.out64[i] = double(xv);
-                if (a.out32) a.out32[i] = xv;
+                if (a.out64) a.out64[i] = double(x[k][t]);
+                if (a.out32) a.out32[i] = x[k][t];
             }
         }
     }
@@ -418,8 +536,7 @@ __global__ __launch_bounds__(kGT) void cg_grid_classic_kernel(Mat A, GridCgArgs 
         int nonconv = 0;
         for (int c = 0; c < C; ++c) nonconv += s_active[c] != 0 ? 1 : 0;
         if (a.st_iters) atomicMax(a.st_iters, it);
-        if (a.st_nonconv && (nonconv || !ok)) atomicAdd(a.st_nonconv, ok ? nonconv : C);
-        if (!ok && a.st_failed) atomicOr(a.st_failed, 1);
+        if (a.st_nonconv && nonconv) atomicAdd(a.st_nonconv, nonconv);
     }
 }
 
@@ -429,7 +546,7 @@ __global__ __launch_bounds__(kGT) void cg_grid_classic_kernel(Mat A, GridCgArgs 
 constexpr int kMaxG = 256;            // workgroups of one pipelined solve (<= one per CU)
 constexpr int kGvMaxRows = 512;       // rows per workgroup: NG x RPG <= 64 x 8
 constexpr int kSyncLine = 32;         // words per sync counter (one 128-B line each)
-constexpr int kSyncWords = 10 * kSyncLine;   // 8 group counters, the top counter, failure word
+constexpr int kSyncWords = 11 * kSyncLine;   // 8 group counters, top counter, failure, rescue
 
 struct GvArgs {
     int m, C, Cp, NQ, PW, max_iter;   // PW: partial floats per workgroup (32 or 64)
@@ -448,6 +565,8 @@ struct GvArgs {
     int32_t* st_iters;
     int32_t* st_nonconv;
     int32_t* st_failed;
+    int32_t* st_rescued;
+    float* rescue;                    // 5 m floats: the rescue solve's vectors
 };
 
 // Grid barrier of the pipelined kernel.  Every wave drains its sc1 stores (asm vmcnt(0):
@@ -871,9 +990,9 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
         ++it;
     }
     GLL_TRACE_PT(10);
-    // a failed grid barrier (a workgroup never arrived within ~1 s) leaves x partial: the
-    // outputs become NaN and GLL_ST_SOLVE_FAILED is raised (see the classic kernel)
-    const float nanf_ = __builtin_nanf("");
+    // a failed grid barrier (a workgroup never arrived within ~1 s): one workgroup solves the
+    // system alone (rescue_solve), the others write nothing
+    if (rescued<Mat, NT>(ok, a.sync + 10 * kSyncLine, A, a, a.rescue, &s_ok)) return;
 #pragma unroll
     for (int k = 0; k < RPG; ++k) {
         const int uu = r0 + grp + k * NG;
@@ -883,9 +1002,8 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
             const int c = 4 * li + t;
             if (c < C) {
                 const size_t i = size_t(uu) * C + c;
-                const float xv = ok ? x[k][t] : nanf_;
-                if (a.out64) a.out64[i] = double(xv);
-                if (a.out32) a.out32[i] = xv;
+                if (a.out64) a.out64[i] = double(x[k][t]);
+                if (a.out32) a.out32[i] = x[k][t];
             }
         }
     }
@@ -893,8 +1011,7 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
         int nonconv = 0;
         for (int c = 0; c < C; ++c) nonconv += s_act[c] != 0 ? 1 : 0;
         if (a.st_iters) atomicMax(a.st_iters, it);
-        if (a.st_nonconv && (nonconv || !ok)) atomicAdd(a.st_nonconv, ok ? nonconv : C);
-        if (!ok && a.st_failed) atomicOr(a.st_failed, 1);
+        if (a.st_nonconv && nonconv) atomicAdd(a.st_nonconv, nonconv);
     }
 }
 
@@ -902,7 +1019,7 @@ size_t grid_cg_workspace_floats(int m, int C) {
     const size_t Cp = size_t((C + 3) & ~3);
     const size_t classic = 64 + size_t(3) * m * Cp + size_t(3) * kGCM * 1024;
     const size_t gv = kSyncWords + size_t(2) * m * Cp + size_t(2) * kMaxG * 64;
-    return classic > gv ? classic : gv;
+    return (classic > gv ? classic : gv) + size_t(5) * m + 64;   // + the rescue vectors
 }
 
 // Workgroups of one kernel instance that can be resident at once on the whole device (the
@@ -916,6 +1033,14 @@ static int coresident_capacity() {
         cap = (nb > 0 ? nb : 1) * device_cus();
     }
     return cap;
+}
+
+// The rescue vectors sit past both grid kernels' regions (grid_cg_workspace_floats).
+static size_t rescue_offset(int m, int C) {
+    const size_t Cp = size_t((C + 3) & ~3);
+    const size_t classic = 64 + size_t(3) * m * Cp + size_t(3) * kGCM * 1024;
+    const size_t gv = kSyncWords + size_t(2) * m * Cp + size_t(2) * kMaxG * 64;
+    return ((classic > gv ? classic : gv) + 63) & ~size_t(63);
 }
 
 // An ordinary launch sized within the co-resident capacity.  MI355X_MICROARCH.md's price list
@@ -943,6 +1068,7 @@ static hipError_t launch_grid(const Mat& A, GridCgArgs a, int G, float* ws, hipS
     a.Pbuf = ws + 64;                                   // 256-B aligned: 16-B buffer accesses
     a.Zbuf = a.Pbuf + size_t(2) * a.m * a.Cp;
     a.part = a.Zbuf + size_t(a.m) * a.Cp;
+    a.rescue = ws + rescue_offset(a.m, a.C);
     hipError_t e = hipMemsetAsync(a.sync, 0, 16, s);
     if (e != hipSuccess) return e;
     return launch_persistent(cg_grid_classic_kernel<Mat, LPR, RPG>, G, kGT, 0, s,
@@ -1012,6 +1138,7 @@ static hipError_t launch_gv(const Mat& A, GvArgs a, int G, int64_t nnz, float* w
     a.sync = reinterpret_cast<unsigned*>(ws);
     a.V = ws + kSyncWords;                       // 1280 B in: 256-B aligned
     a.part = a.V + size_t(2) * a.m * a.Cp;
+    a.rescue = ws + rescue_offset(a.m, a.C);
     a.lds_cap = int(lds / 8);
     hipError_t e = hipMemsetAsync(a.sync, 0, kSyncWords * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
@@ -1045,6 +1172,7 @@ static hipError_t dispatch_gv(const Mat& A, const GridCgArgs& c, int64_t nnz, fl
     a.st_iters = c.st_iters;
     a.st_nonconv = c.st_nonconv;
     a.st_failed = c.st_failed;
+    a.st_rescued = c.st_rescued;
     a.hier = 1;   // XCD-class hierarchical arrivals (a flat counter measured 116 against 74 us)
     int cap = std::min(kMaxG, device_cus());
     if (knob(GLL_KNOB_GRID_CAP) > 0) cap = std::min(cap, knob(GLL_KNOB_GRID_CAP));
@@ -1106,6 +1234,8 @@ hipError_t launch_cg_grid_luu(const Layout& L, void* wsp, const void* b, int b_d
     a.st_iters = st_iters;
     a.st_nonconv = st_nonconv;
     a.st_failed = st_failed;
+    // the public words are one array (include/gll.h): GLL_ST_GRID_RESCUED beside SOLVE_FAILED
+    a.st_rescued = st_failed ? st_failed - GLL_ST_SOLVE_FAILED + GLL_ST_GRID_RESCUED : nullptr;
     a.diag_fail = (L.flags & GLL_FLAG_DIAG_GRID_FAIL) ? 1 : 0;
     // U-block entries per row ~ 1.5 (K-1) m / n on kNN graphs (union rows, U share)
     const int64_t nnz_est = int64_t(double(L.m) * (L.K - 1) * 1.5 * double(L.m) / double(L.n)) + L.m;
@@ -1131,6 +1261,7 @@ hipError_t launch_cg_grid_csr(int m, int C, const int32_t* row_ptr, const int32_
     a.st_iters = iters;
     a.st_nonconv = nonconv;
     a.st_failed = failed;
+    a.st_rescued = failed ? failed - GLL_ST_SOLVE_FAILED + GLL_ST_GRID_RESCUED : nullptr;
     return dispatch_grid(A, a, nnz, ws, false, s);
 }
 

@@ -95,8 +95,13 @@ DeviceStatus& status_of(int dev) {
 void report(const int32_t* st) {
     if (st[GLL_ST_SOLVE_FAILED])
         raise_py(PyExc_RuntimeError,
-                 "GLL: a whole-GPU CG solve lost a grid barrier (a workgroup never arrived); "
-                 "its outputs were written as NaN");
+                 "GLL: the fused backward's gradient gave up waiting for the adjoint solves; "
+                 "its grad_X was written as NaN");
+    if (st[GLL_ST_GRID_RESCUED])
+        warn_py(PyExc_RuntimeWarning,
+                "GLL: " + std::to_string(st[GLL_ST_GRID_RESCUED]) +
+                    " whole-GPU CG solve(s) lost their grid barrier (other kernels held the "
+                    "CUs) and were solved by one workgroup instead: correct, slower");
     if (st[GLL_ST_TINY_EPS]) warn_py(PyExc_UserWarning, "Epsilon in KNN is very close to zero.");
     if (st[GLL_ST_FWD_NONCONV])
         warn_py(PyExc_RuntimeWarning,

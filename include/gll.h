@@ -42,11 +42,15 @@ extern "C" {
 #define GLL_ST_KNN_RESCAN 5    /* kNN rows whose candidate set failed the Gram error certificate
                                 * and were re-ranked exactly over every column under the bound
                                 * (diagnostic count; the result is exact either way) */
-#define GLL_ST_SOLVE_FAILED 6  /* nonzero: a whole-GPU CG lost a grid barrier (a workgroup never
-                                * arrived); that solve's outputs were written as NaN.  The
-                                * Python layer raises RuntimeError on it */
+#define GLL_ST_SOLVE_FAILED 6  /* nonzero: the fused backward's gradient workgroups gave up
+                                * waiting for the adjoint solves (~1 s); the gradient was written
+                                * as NaN.  The Python layer raises RuntimeError on it */
 #define GLL_ST_KNN_MERGE 7     /* kNN rows whose short candidate lists may have dropped a column:
                                 * the exact merge ran instead (diagnostic count) */
+                               /* (words 8, 9 are internal) */
+#define GLL_ST_GRID_RESCUED 10 /* whole-GPU CG solves whose grid barrier timed out (a workgroup
+                                * was not resident: other kernels held the CUs) and that one
+                                * workgroup then solved alone -- correct, slower (count) */
 #define GLL_ST_NWORDS 16
 
 /* gll_problem.flags: code-path choices for tests and A/B runs; none changes a result beyond
@@ -57,7 +61,7 @@ extern "C" {
                                         * far past its co-resident capacity -- the launch must
                                         * be refused */
 #define GLL_FLAG_DIAG_GRID_FAIL 256    /* tests: inject a grid-barrier failure into the
-                                        * whole-GPU CG (NaN outputs + GLL_ST_SOLVE_FAILED) */
+                                        * whole-GPU CG (the rescue solve takes over) */
 #define GLL_FLAG_CG_ELL 512     /* per-column CG: register-ELL kernel even where the balanced
                                  * (virtual-row) kernel would run */
 #define GLL_FLAG_CG_VR 1024     /* per-column CG: balanced (virtual-row) kernel wherever it can
