@@ -98,8 +98,10 @@ inline int vr_threads(int n, int m, int K, int flags) {
     }                                                                                        \
     struct TraceScope {                                                                      \
         int k;                                                                               \
+        /* sampled (every 16th workgroup): a global atomic per workgroup of a 640-workgroup   \
+           launch serialises at the memory side and distorts what it measures */              \
         __device__ explicit TraceScope(int k_) : k(k_) {                                     \
-            if (threadIdx.x == 0) {                                                          \
+            if (threadIdx.x == 0 && ((blockIdx.x | blockIdx.y) & 15) == 0) {                 \
                 const unsigned long long t = __builtin_amdgcn_s_memrealtime();               \
                 atomicMin(&g_trace[32 + 2 * k], t);                                          \
                 atomicMax(&g_trace[24 + k], t);                                              \
@@ -110,7 +112,7 @@ inline int vr_threads(int n, int m, int K, int flags) {
             }                                                                                \
         }                                                                                    \
         __device__ ~TraceScope() {                                                           \
-            if (threadIdx.x == 0) {                                                          \
+            if (threadIdx.x == 0 && ((blockIdx.x | blockIdx.y) & 15) == 0) {                 \
                 const unsigned long long t = __builtin_amdgcn_s_memrealtime();               \
                 atomicMax(&g_trace[33 + 2 * k], t);                                          \
                 if (k < 2 && blockIdx.x < 4096 && blockIdx.y == 0)                           \

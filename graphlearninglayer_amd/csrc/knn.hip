@@ -2013,39 +2013,58 @@ __device__ __forceinline__ int pivot_row(int j, int n) {
     return int((uint32_t(j) * 2654435761u + 12345u) % uint32_t(n));
 }
 
+// 64 rows per workgroup, the pivots split over its 4 waves (16 each: every load of a lane
+// issued together), the 4 partial minima combined in LDS in pivot order.
 template <int NP>
 __global__ __launch_bounds__(256) void order_pid_kernel(const float* __restrict__ D2, int ld,
                                                         size_t plane, int n,
                                                         int32_t* __restrict__ pid,
                                                         int32_t* __restrict__ status) {
-    const int i = int(blockIdx.x) * 256 + int(threadIdx.x);
-    if (i >= n) return;
-    float v[kPiv];
+    constexpr int PPW = kPiv / 4;   // pivots per wave
+    __shared__ float s_best[4][kWave];
+    __shared__ int s_arg[4][kWave];
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    const int i = int(blockIdx.x) * kWave + lane;
+    const int ic = i < n ? i : n - 1;
+    float v[PPW];
 #pragma unroll
-    for (int j = 0; j < kPiv; ++j) {   // every load issued before any is compared
-        const size_t o = size_t(pivot_row(j, n)) * ld + i;
+    for (int j = 0; j < PPW; ++j) {   // every load issued before any is compared
+        const size_t o = size_t(pivot_row(wv * PPW + j, n)) * ld + ic;
         v[j] = D2[o];
 #pragma unroll
         for (int p = 1; p < NP; ++p) v[j] += D2[p * plane + o];
     }
     float best = __builtin_inff();
-    int bp = 0;
+    int bp = wv * PPW;
 #pragma unroll
-    for (int j = 0; j < kPiv; ++j)
-        if (v[j] < best) {
+    for (int j = 0; j < PPW; ++j)
+        if (v[j] < best) {   // ties: the lower pivot; a NaN never wins
             best = v[j];
-            bp = j;
+            bp = wv * PPW + j;
         }
-    pid[i] = bp;
-    atomicAdd(&status[kStPiv + bp], 1);
+    s_best[wv][lane] = best;
+    s_arg[wv][lane] = bp;
+    __syncthreads();
+    if (wv == 0 && i < n) {
+#pragma unroll
+        for (int w = 1; w < 4; ++w)
+            if (s_best[w][lane] < best) {
+                best = s_best[w][lane];
+                bp = s_arg[w][lane];
+            }
+        pid[i] = bp;
+        atomicAdd(&status[kStPiv + bp], 1);
+    }
 }
 
 // One workgroup: the pivots' row counts -> offsets (wave 0's scan), then every row to its
-// pivot's range (LDS cursors; the order inside a range is arbitrary -- speed only).
+// pivot's range (LDS cursors; the order inside a range is arbitrary -- speed only).  Each
+// thread's pivot ids are all loaded before its first cursor atomic.
 __global__ __launch_bounds__(1024) void order_perm_kernel(int n, const int32_t* __restrict__ pid,
                                                           const int32_t* __restrict__ status,
                                                           int32_t* __restrict__ perm) {
     static_assert(kPiv == kWave, "one wave scans the pivot counts");
+    constexpr int U = 8;
     __shared__ int base[kPiv];
     __shared__ int cur[kPiv];
     const int tid = threadIdx.x;
@@ -2061,9 +2080,16 @@ __global__ __launch_bounds__(1024) void order_perm_kernel(int n, const int32_t* 
         cur[tid] = 0;
     }
     __syncthreads();
-    for (int i = tid; i < n; i += 1024) {
-        const int p = pid[i];
-        perm[base[p] + atomicAdd(&cur[p], 1)] = i;
+    for (int i0 = 0; i0 < n; i0 += 1024 * U) {
+        int p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * 1024 + tid;
+            p[u] = i < n ? pid[i] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (p[u] >= 0) perm[base[p[u]] + atomicAdd(&cur[p[u]], 1)] = i0 + u * 1024 + tid;
     }
 }
 
@@ -2072,7 +2098,7 @@ hipError_t launch_order(const Layout& L, void* ws, hipStream_t s) {
     int32_t* st = L.at<int32_t>(ws, L.status);
     int32_t* pid = L.at<int32_t>(ws, L.pid);
     const size_t plane = size_t(L.n) * L.ldD;
-    const dim3 grid(unsigned((L.n + 255) / 256));
+    const dim3 grid(unsigned((L.n + kWave - 1) / kWave));
     if (gram_planes(L, 1) == 2)
         launch_k(order_pid_kernel<2>, grid, 256, 0, s, D2, L.ldD, plane, L.n, pid, st);
     else

@@ -957,7 +957,9 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
     if (cap > kOvfLds) cap = kOvfLds;
     if (cap < 0) cap = 0;
     lds += size_t(cap) * 8;
-    if (S != ell_emit(L, bt.B)) return hipErrorInvalidValue;   // row_build emitted ell_emit(L, B)
+    // the kernel holds the first S of the ell_emit(L, B) slots row_build wrote in registers
+    // (entries past S come from the CSR through the LDS overflow)
+    if (S > ell_emit(L, bt.B)) return hipErrorInvalidValue;
     auto fn = cg_ell_kernel<NT, R, S, TB, MODE>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
     launch_k(fn, dim3(L.C, bt.B), NT, lds, s, 
@@ -1319,6 +1321,25 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     // workgroup -- measured slower at B = 64 and 8 and were removed in round 4:
     // profiles/r03s_cg_pairs_ab.txt.)
     if (m <= 512 && (bt.B == 1 || int64_t(bt.B) * L.C <= 256)) GLL_ELL(512, 1, 24);
+    if (m <= 512 && knob(GLL_KNOB_CG_GEOM) > 0) {
+        // batched geometry A/B (tests / tools/ab_flags.py --knob): threads x rows per thread,
+        // ELL slots held in registers, and the recurrence (1 single-reduction, 3 Neumann-1)
+#define GLL_ELLM(NT, R, S, MODE) \
+        return run_ell<NT, R, S, TB, MODE>(L, bt, ws, b, bs, out64, out32, rtol, max_iter, st_nonconv, st_iters, s)
+        switch (knob(GLL_KNOB_CG_GEOM)) {
+            case 1: GLL_ELLM(256, 2, 24, 1);
+            case 2: GLL_ELLM(512, 1, 24, 3);
+            case 3: GLL_ELLM(256, 2, 24, 3);
+            case 4: GLL_ELLM(256, 2, 16, 3);
+            case 5: GLL_ELLM(256, 2, 12, 3);
+            case 6: GLL_ELLM(256, 2, 12, 1);
+            case 7: GLL_ELLM(128, 4, 12, 1);
+            case 8: GLL_ELLM(512, 1, 12, 3);
+            case 9: GLL_ELLM(512, 1, 8, 1);
+            default: break;
+        }
+#undef GLL_ELLM
+    }
     if (m <= 512) GLL_ELL(256, 2, 24);
     if (m <= 1024) GLL_ELL(1024, 1, 16);
     if (m <= 2048) GLL_ELL(1024, 2, 16);

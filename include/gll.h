@@ -92,7 +92,8 @@ extern "C" {
 #define GLL_KNOB_VR_RV 0      /* balanced CG: virtual rows per thread (4 / 8 / 10) */
 #define GLL_KNOB_GRID_CAP 1   /* whole-GPU CG: co-resident workgroup capacity */
 #define GLL_KNOB_GRAM_TILE 2  /* pre-split Gram: 128- or 256-row tiles */
-#define GLL_KNOB_COUNT 3
+#define GLL_KNOB_CG_GEOM 3    /* batched per-column CG geometry variant (A/B; solve.hip) */
+#define GLL_KNOB_COUNT 4
 int gll_set_knob(int knob, int value);
 
 typedef struct gll_problem {

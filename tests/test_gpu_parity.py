@@ -1087,3 +1087,27 @@ def test_locality_order_changes_no_result(eps):
     U1, g1 = _fwd_bwd_c_abi(X, Y, c["k"], 0.07, eps, g, flags=_lib.FLAG_ROW_ORDER_OFF)
     np.testing.assert_array_equal(U0, U1)
     np.testing.assert_array_equal(g0, g1)
+
+
+def test_batched_cg_geometry_variants_match_oracle():
+    """The batched per-column CG geometries selectable for A/B runs (GLL_KNOB_CG_GEOM: threads x
+    rows per thread, ELL slots in registers -- entries past them from the CSR through the LDS
+    overflow -- and the single-reduction or Neumann-1 recurrence) all solve the same systems:
+    every variant within 1e-5 of the automatic choice and the oracle's 1e-4 bar (GLL.py:53,93)."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import seeded_gbar
+    B = 40   # B x C > 256: the batched geometry
+    Xs, Ys, c = _synth_batch("ns", B, seed0=61)
+    G = np.stack([seeded_gbar(c["batch"], 10, 800 + g) for g in range(B)])
+    U0, g0 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G)
+    ind = _gpu_knn(Xs[3], c["k"], 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, st = O.forward(Xs[3], Ys[3], tau=0.07, epsilon=1.0, K=c["k"], knn=(ind, None))
+    go = O.backward(st, G[3])
+    try:
+        for geom in range(1, 10):
+            _lib.set_knob(_lib.KNOB_CG_GEOM, geom)
+            U1, g1 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G)
+            assert O.rel_err(U1, U0) <= 1e-5 and O.rel_err(g1, g0) <= 1e-5, geom
+            assert O.rel_err(U1[3], Uo) <= TOL and O.rel_err(g1[3], go) <= TOL, geom
+    finally:
+        _lib.set_knob(_lib.KNOB_CG_GEOM, 0)
