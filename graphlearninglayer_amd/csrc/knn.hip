@@ -902,29 +902,6 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
 // --------------------------------------------------------------------------------------
 // K1b: per-row selection + exact re-rank + reverse scatter
 // --------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t pack_key(float d2, int j) {
-    // d2 >= 0 after the clamp, so its IEEE bits order like the value; index breaks ties
-    return (uint64_t(__float_as_uint(d2 > 0.f ? d2 : 0.f)) << 32) | uint32_t(j);
-}
-
-template <int KC>
-__device__ __forceinline__ void list_insert(uint64_t (&key)[KC], uint64_t v) {
-    // precondition: v < key[KC-1]; ascending order kept (keys are unique)
-#pragma unroll
-    for (int t = KC - 1; t > 0; --t) {
-        const uint64_t prev = key[t - 1];
-        key[t] = prev > v ? prev : (key[t] > v ? v : key[t]);
-    }
-    key[0] = key[0] > v ? v : key[0];
-}
-
-template <int KC>
-__device__ __forceinline__ void list_pop(uint64_t (&key)[KC], bool pop) {
-#pragma unroll
-    for (int t = 0; t < KC - 1; ++t) key[t] = pop ? key[t + 1] : key[t];
-    key[KC - 1] = pop ? ~0ull : key[KC - 1];
-}
-
 // A row of D2 as the select reads it: fp32, or fp16 x s decoded x 1/s (H, the pre-split route;
 // 1/s is a power of two, so decoding adds no rounding).  Element offsets, 4-aligned for ld4.
 template <bool H>
@@ -944,51 +921,6 @@ struct D2Row {
         else return *reinterpret_cast<const float*>(base + 4 * e);
     }
 };
-
-// Per-lane scan of row i of D2 (the sum of NP partial planes, added in plane order) into a
-// sorted list of the lane's KC smallest keys; returns how many valid columns the lane saw.
-// NB float4 per lane and plane are loaded before any is consumed (one memory latency per
-// 256*NB columns); addresses past the row are clamped, not branched around.
-template <int KC, int NP, bool H = false>
-__device__ __forceinline__ int scan_row(const D2Row<H>& row, size_t plane, int n,
-                                        int ld, int i, uint64_t (&key)[KC]) {
-    constexpr int NB = 4;
-    const int lane = lane_id();
-#pragma unroll
-    for (int t = 0; t < KC; ++t) key[t] = ~0ull;
-    int seen = 0;
-    for (int jb = 0; jb < n; jb += 4 * kWave * NB) {
-        f32x4 v[NB];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const int j0 = jb + 4 * (b * kWave + lane);
-            const int jc = j0 < ld ? j0 : 0;
-            v[b] = row.ld4(jc);
-#pragma unroll
-            for (int p = 1; p < NP; ++p) v[b] += row.ld4(p * plane + jc);
-        }
-#ifdef GLL_TRACE
-        if (jb == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (blockIdx.x == 0 && threadIdx.x == 0) g_trace[23] = __builtin_amdgcn_s_memrealtime();
-        }
-#endif
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const int j0 = jb + 4 * (b * kWave + lane);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int j = j0 + t;
-                if (j < n && j != i && v[b][t] == v[b][t]) {   // NaN rows never enter
-                    ++seen;
-                    const uint64_t kv = pack_key(v[b][t], j);
-                    if (kv < key[KC - 1]) list_insert<KC>(key, kv);
-                }
-            }
-        }
-    }
-    return seen;
-}
 
 // Wave64 minimum of a 32-bit unsigned key through DPP (broadcast result).
 template <int CTRL, int ROW_MASK>
@@ -1021,122 +953,16 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-// Exact merge (fallback): round t hands the t-th smallest (d2, index) key to lane t.
-// `tb` receives the D2 bits of the kc-th key (every column left out is >= it), or +inf when
-// fewer than kc valid columns exist (then every one of them is a candidate).
-template <int KC>
-__device__ __forceinline__ int merge_exact(uint64_t (&key)[KC], int kc, uint32_t& tb,
-                                           uint32_t& gbits) {
-    const int lane = lane_id();
-    uint64_t mine = ~0ull;
-    tb = 0x7F800000u;
-    for (int t = 0; t < kc; ++t) {
-        const uint64_t best = wave_min_u64(key[0]);
-        if (lane == t) mine = best;
-        if (best != ~0ull && t == kc - 1) tb = uint32_t(best >> 32);
-        list_pop<KC>(key, best != ~0ull && key[0] == best);
-    }
-    gbits = uint32_t(mine >> 32);
-    return mine == ~0ull ? -1 : int(uint32_t(mine));
-}
-
-// Fast merge: 32-bit DPP arg-min on (value bits with the lane id in the 6 low bits).  The
-// candidate SET can differ from the exact one only between values within 64 ulp of each
-// other, which the exact re-rank margin absorbs.  Returns true when some lane emptied its
-// list while holding more columns (the set may then miss one): the caller re-runs exactly.
-template <int KS>
-__device__ __forceinline__ bool merge_fast(uint64_t (&key)[KS], int kc, int seen, int& ci) {
-    const int lane = lane_id();
-    int popped = 0;
-    ci = -1;
-    for (int t = 0; t < kc; ++t) {
-        const uint32_t hi = uint32_t(key[0] >> 32);
-        const uint32_t packed = key[0] == ~0ull ? 0xFFFFFFFFu : ((hi & ~63u) | uint32_t(lane));
-        const uint32_t m = wave_min_u32(packed);
-        if (m == 0xFFFFFFFFu) break;
-        const int wl = int(m & 63u);
-        const int idx = __builtin_amdgcn_readlane(int(uint32_t(key[0])), wl);
-        if (lane == t) ci = idx;
-        const bool pop = lane == wl;
-        list_pop<KS>(key, pop);
-        popped += pop ? 1 : 0;
-    }
-    return __ballot(popped == KS && seen > KS) != 0;
-}
-
-// Threshold merge: T = the kc-th smallest 32-bit key head (the D2 bits) over all lanes' lists,
-// by bisection -- each step is KS ballots and scalar popcounts, no DPP chain (~0.4 us against
-// ~2 us for kc arg-min rounds at NS).  Every list entry <= T is a candidate, ties at T
-// included, so the set is exact on the D2 values (at most 64).  Returns true when it may be
-// incomplete: some lane's whole list is <= T while that lane saw more columns, or more than 64
-// candidates tie in; the caller then re-runs the exact merge.
-template <int KS>
-__device__ __forceinline__ bool merge_threshold(const uint64_t (&key)[KS], int kc, int seen,
-                                                int* __restrict__ cand,
-                                                uint32_t* __restrict__ cgd, int& ci, int& kce,
-                                                uint32_t& tb, uint32_t& gbits) {
-    const int lane = lane_id();
-    uint32_t hv[KS];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) hv[s] = uint32_t(key[s] >> 32);   // empty slots: 0xFFFFFFFF
-    auto count_le = [&](uint32_t t) {
-        int c = 0;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) c += __popcll(__ballot(hv[s] <= t));
-        return c;
-    };
-    // T lies between the smallest list head and, when at least kc entries are that small, the
-    // largest head: a bracket of ~2^24 instead of 2^32 (8 fewer steps at NS)
-    uint32_t lo = wave_min_u32(hv[0]), up = 0xFFFFFFFEu;
-    const uint32_t hmax = wave_max_u32(hv[0] == 0xFFFFFFFFu ? 0u : hv[0]);
-    if (lo > up) lo = up;   // every list empty
-    if (hmax >= lo && count_le(hmax) >= kc) up = hmax;
-    tb = 0x7F800000u;        // fewer than kc valid entries: all of them are candidates
-    if (count_le(up) >= kc) {
-        while (lo < up) {   // smallest T with count_le(T) >= kc (wave-uniform, <= 32 steps)
-            const uint32_t mid = lo + ((up - lo) >> 1);
-            if (count_le(mid) >= kc) up = mid;
-            else lo = mid + 1u;
-        }
-        tb = up;             // the kc-th smallest D2: every column left out is > it
-    }
-    const uint32_t T = up;
-    const uint64_t below = (1ull << lane) - 1ull;
-    int mine = 0, before = 0, total = 0;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        const uint64_t mk = __ballot(hv[s] <= T);
-        mine += hv[s] <= T ? 1 : 0;
-        before += __popcll(mk & below);
-        total += __popcll(mk);
-    }
-    const bool redo = (__ballot(mine == KS && seen > KS) != 0) || total > kWave;
-    if (!redo) {   // a lane's entries <= T are a prefix of its sorted list
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-            if (hv[s] <= T) {
-                cand[before + s] = int(uint32_t(key[s]));
-                cgd[before + s] = hv[s];
-            }
-    }
-    __builtin_amdgcn_wave_barrier();   // a wave's LDS ops run in order: the reads see the stores
-    asm volatile("" ::: "memory");
-    kce = total;
-    ci = (!redo && lane < total) ? cand[lane] : -1;
-    gbits = (!redo && lane < total) ? cgd[lane] : 0xFFFFFFFFu;
-    return redo;
-}
-
-// Threshold scan (round 3; replaces scan_row + merge_threshold for kc <= 32): each lane keeps
-// only its TOP smallest D2 bits (min/max network, ~2 VALU per slot, against the ~35 of a sorted
-// 64-bit list insert: the batched select was VALU-issue bound), T = the kc-th smallest of the
-// 64 x TOP lane entries by bisection -- at least kc distinct columns are <= T, so the kc-th
-// smallest D2 is too -- and every column with D2 bits <= T is compacted into the wave's LDS
-// slots in column order.  Simulated at kc = 13 / n = 1,000 (TOP = 2) the set averages 13.2
-// columns, at kc = 32 / n = 1,500 (TOP = 3) 32.4.  CH > 0: the row (n <= 1024 CH) stays in
-// registers between the two passes; CH = 0 re-reads it (L1/L2-hot).  Returns true when more
-// than 64 columns tie in (the caller re-runs the exact merge).  tb: D2 bits every left-out
-// column is >= to (+inf when every valid column is a candidate).
+// Threshold scan: each lane keeps only its TOP smallest D2 bits (min/max network, ~2 VALU per
+// slot, against the ~35 of the sorted 64-bit list insert it replaced -- that select was VALU-issue
+// bound), T = the kc-th smallest of the 64 x TOP lane entries by bisection -- at least kc distinct
+// columns are <= T, so the kc-th smallest D2 is too -- and every column with D2 bits <= T is
+// compacted into the wave's LDS slots.  Simulated at kc = 13 / n = 1,000 (TOP = 2) the set
+// averages 13.2 columns, at kc = 32 / n = 1,500 (TOP = 3) 32.4; kc = 37 / n = 8,192 (stress,
+// TOP = 4) holds ~0.6 of the kc nearest per lane.  CH > 0: the row (n <= 1024 CH) stays in
+// registers between the two passes; CH = 0 re-reads it (L2 / MALL-hot).  Returns true when more
+// than 64 columns tie in (the caller runs select_fallback, tb = T on return).  tb: D2 bits every
+// left-out column is >= to (+inf when every valid column is a candidate).
 constexpr int kSelNB = 4;   // float4 per lane per 1024-column chunk of a D2 row
 
 // Loads of CH 1024-column chunks of D2 row `row` (sum of NP planes), clamped past ld.
@@ -1273,13 +1099,97 @@ __device__ __forceinline__ bool select_threshold(const D2Row<H>& row, size_t pla
         }
     }
     const bool redo = base > kWave;
-    tb = __ballot(mine != nvalid) == 0 ? 0x7F800000u : T + 1u;
+    tb = redo ? T : (__ballot(mine != nvalid) == 0 ? 0x7F800000u : T + 1u);
     __builtin_amdgcn_wave_barrier();   // a wave's LDS ops run in order: the reads see the stores
     asm volatile("" ::: "memory");
     kce = base;
     ci = (!redo && lane < base) ? cand[lane] : -1;
     gbits = (!redo && lane < base) ? cgd[lane] : 0xFFFFFFFFu;
     return redo;
+}
+
+// Fallback of the threshold scan when more than 64 columns have D2 bits <= T (ties: duplicate
+// points): T' = the kc-th smallest D2 bits of the whole row, by bisection on full-row counts in
+// [0, T] (the scan's T already has >= kc columns at or below it; <= 31 passes over the hot row,
+// rare), then every column below T' -- fewer than kc -- and columns at T' in index order up to
+// 64 slots.  Every column left out is >= T' (tb).  Registers: the scan's, no per-lane key lists
+// (the 64-key exact merge it replaces held 128 VGPRs and set the select's occupancy).
+template <int NP, bool H = false>
+__device__ __forceinline__ void select_fallback(const D2Row<H>& row, size_t plane, int n, int ld,
+                                                int i, int kc, int* __restrict__ cand,
+                                                uint32_t* __restrict__ cgd, int& ci, int& kce,
+                                                uint32_t& tb, uint32_t& gbits) {
+    constexpr int NB = kSelNB;
+    const int lane = lane_id();
+    auto bits_of = [&](float x, int j) -> uint32_t {
+        return (j < n && j != i && x == x) ? __float_as_uint(x > 0.f ? x : 0.f) : 0xFFFFFFFFu;
+    };
+    auto wave_count_le = [&](uint32_t thr) {   // wave-uniform
+        int c = 0;
+        for (int jb = 0; jb < n; jb += 4 * kWave * NB) {
+            f32x4 v[NB];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const int j0 = jb + 4 * (b * kWave + lane);
+                const int jc = j0 < ld ? j0 : 0;
+                v[b] = row.ld4(jc);
+#pragma unroll
+                for (int p = 1; p < NP; ++p) v[b] += row.ld4(p * plane + jc);
+            }
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    c += __popcll(__ballot(bits_of(v[b][t], jb + 4 * (b * kWave + lane) + t) <= thr));
+        }
+        return c;
+    };
+    uint32_t lo = 0u, up = tb;   // count_le(tb) >= kc (select_threshold's T)
+    while (lo < up) {   // smallest T' with count_le(T') >= kc (wave-uniform)
+        const uint32_t mid = lo + ((up - lo) >> 1);
+        if (wave_count_le(mid) >= kc) up = mid;
+        else lo = mid + 1u;
+    }
+    const uint32_t T = up;
+    // columns below T' (any order), then ties at T' in index order: lane-contiguous columns
+    int base = 0;
+    auto emit = [&](bool p, uint32_t u, int j) {
+        const uint64_t mk = __ballot(p);
+        const int pos = base + lanes_below(mk);
+        if (p && pos < kWave) {
+            cand[pos] = j;
+            cgd[pos] = u;
+        }
+        base += __popcll(mk);
+    };
+    for (int j0 = 0; j0 < n; j0 += kWave) {
+        const int j = j0 + lane;
+        float x = 0.f;
+        if (j < n) {
+            x = row.ld1(j);
+#pragma unroll
+            for (int p = 1; p < NP; ++p) x += row.ld1(p * plane + j);
+        }
+        const uint32_t u = bits_of(x, j);
+        emit(u < T, u, j);
+    }
+    for (int j0 = 0; j0 < n && base < kWave; j0 += kWave) {
+        const int j = j0 + lane;
+        float x = 0.f;
+        if (j < n) {
+            x = row.ld1(j);
+#pragma unroll
+            for (int p = 1; p < NP; ++p) x += row.ld1(p * plane + j);
+        }
+        const uint32_t u = bits_of(x, j);
+        emit(u == T, u, j);
+    }
+    tb = T;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    kce = base < kWave ? base : kWave;
+    ci = lane < kce ? cand[lane] : -1;
+    gbits = lane < kce ? cgd[lane] : 0xFFFFFFFFu;
 }
 
 // 64-bit DPP add of the 8-lane group butterfly (two 32-bit moves per stage).
@@ -1552,39 +1462,23 @@ void knn_select_kernel(
     // bounds between a true Gram value v and its stored decoding t: |t - v| <= rho |v| + sub
     auto up = [&](double t) { return H ? t + 2.0 * rho * fabs(t) + sub : t; };   // >= v
     auto lo = [&](double t) { return H ? t - 2.0 * rho * fabs(t) - sub : t; };   // <= v
-    constexpr int KS = KC <= 16 ? 4 : 8;
     int ci, kce;
     uint32_t tb, gb;   // gb: this lane's candidate's Gram D2 bits
     {
-        bool redo;
-        if constexpr (KC <= 32) {
-            f32x4 vrow[CH > 0 ? CH * kSelNB : 1];
-            if constexpr (CH > 0) load_d2_row<NP, CH, H>(row, plane, ld, vrow);
-            redo = select_threshold<KC == 16 ? 2 : 3, NP, CH, H>(row, plane, n, ld, i, kc, s_cand[wv],
-                                                              s_cgd[wv], ci, kce, tb, gb, vrow);
-            if constexpr (XL) {
+        f32x4 vrow[CH > 0 ? CH * kSelNB : 1];
+        if constexpr (CH > 0) load_d2_row<NP, CH, H>(row, plane, ld, vrow);
+        constexpr int TOP = KC == 16 ? 2 : (KC == 32 ? 3 : 4);
+        const bool redo = select_threshold<TOP, NP, CH, H>(row, plane, n, ld, i, kc, s_cand[wv],
+                                                           s_cgd[wv], ci, kce, tb, gb, vrow);
+        if constexpr (XL) {
 #pragma unroll
-                for (int q = 0; q < XQ; ++q)
-                    *reinterpret_cast<f32x4*>(&s_xi[wv][4 * lane + 256 * q]) = xr[q];
-            }
-        } else {
-            uint64_t key[KS];
-            const int seen = scan_row<KS, NP, H>(row, plane, n, ld, i, key);
-            GLL_TRACE_PT(16);
-            if constexpr (XL) {
-#pragma unroll
-                for (int q = 0; q < XQ; ++q)
-                    *reinterpret_cast<f32x4*>(&s_xi[wv][4 * lane + 256 * q]) = xr[q];
-            }
-            redo = merge_threshold<KS>(key, kc, seen, s_cand[wv], s_cgd[wv], ci, kce, tb, gb);
+            for (int q = 0; q < XQ; ++q)
+                *reinterpret_cast<f32x4*>(&s_xi[wv][4 * lane + 256 * q]) = xr[q];
         }
         GLL_TRACE_PT(17);
         if (redo) {
             if (lane == 0) atomicAdd(&status_pub[GLL_ST_KNN_MERGE], 1);
-            uint64_t full[KC];
-            scan_row<KC, NP, H>(row, plane, n, ld, i, full);
-            ci = merge_exact<KC>(full, kc, tb, gb);
-            kce = kc;
+            select_fallback<NP, H>(row, plane, n, ld, i, kc, s_cand[wv], s_cgd[wv], ci, kce, tb, gb);
         }
     }
     // 2b) drop the candidates the Gram's error bound already rules out, before their exact
@@ -2227,6 +2121,13 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     const float* d2s = L.at<float>(ws, L.d2s);
     const int32_t* perm = (locality_order(L, bt) && r0 == 0 && rows == n)
                               ? L.at<int32_t>(ws, L.perm) : nullptr;
+    // the latency form (PG = 2 candidate groups in flight, NU = 16, ~200 VGPRs: 2 waves per SIMD)
+    // for a single graph whose rows fill at most one such round of the chip; larger graphs (and
+    // batches) run the occupancy form below.  Stress (n = 8,192): 2,048 workgroups, four rounds
+    // of the latency form (profiles/r04c_trace_stress.txt: the last workgroup starts at +200 of
+    // 255 us).  GLL_KNOB_SEL_FORM 1 / 2 forces either (tests, A/B).
+    const int form = knob(GLL_KNOB_SEL_FORM);
+    const bool lat = bt.B == 1 && (form == 1 || (form == 0 && rows <= 2048));
     prof_begin(GLL_K_SELECT, s);
 // Batched launches (PG = 1) stage x_i in LDS (XQ quarters of 256 features, d <= 1024) and run at
 // 6 waves per SIMD: measured at B = 64 NS, select 259 -> 214 us (XQ = 2, NU = 8; the NU = 16
@@ -2237,7 +2138,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
 // graphs): NS B = 64 220 -> 213 us, FullySup B = 64 440 -> 429 us (profiles/r02h_xcd_ab.txt),
 // once the kernel took its graph index once instead of per pointer.
 #define GLL_SEL6(KCV, V, NPV, NUS, NUB, XQV, CHV, HV)                                          \
-    launch_k((bt.B == 1 ? knn_select_kernel<KCV, V, NPV, 2, NUS, 0, false, CHV, HV>            \
+    launch_k((lat ? knn_select_kernel<KCV, V, NPV, 2, NUS, 0, false, CHV, HV>            \
                         : knn_select_kernel<KCV, V, NPV, 1, NUB, (V ? XQV : 0), true, CHV, HV>), grid, 256, 0, s, \
         L.at<float>(ws, L.D2), L.ldD, plane, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0,     \
         L.RCAP,                                                                                \

@@ -1317,29 +1317,13 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     // at most one column workgroup per CU (B x C <= 256) run the single-graph geometry, 512 x 1
     // with the Neumann form: NS B = 8 18.6 -> 15.9 us per launch; with more workgroups than CUs
     // 256 x 2 (MODE 1) keeps the lead: B = 64 21.9 against 28.2 us
-    // (profiles/r03t_cg_batched_geometry_ab.txt).  (Column pairs -- two right-hand sides per
+    // (profiles/r03t_cg_batched_geometry_ab.txt).  Round 4 swept nine batched geometries (128 /
+    // 256 / 512 threads x 4 / 2 / 1 rows, 8-24 register ELL slots, MODE 1 and 3) at B = 64:
+    // none beat 256 x 2 x 24 MODE 1 (21.9 us; the best Neumann form 28.2 us,
+    // profiles/r04c_ab_geom.txt), and the variants were removed.  (Column pairs -- two right-hand sides per
     // workgroup -- measured slower at B = 64 and 8 and were removed in round 4:
     // profiles/r03s_cg_pairs_ab.txt.)
     if (m <= 512 && (bt.B == 1 || int64_t(bt.B) * L.C <= 256)) GLL_ELL(512, 1, 24);
-    if (m <= 512 && knob(GLL_KNOB_CG_GEOM) > 0) {
-        // batched geometry A/B (tests / tools/ab_flags.py --knob): threads x rows per thread,
-        // ELL slots held in registers, and the recurrence (1 single-reduction, 3 Neumann-1)
-#define GLL_ELLM(NT, R, S, MODE) \
-        return run_ell<NT, R, S, TB, MODE>(L, bt, ws, b, bs, out64, out32, rtol, max_iter, st_nonconv, st_iters, s)
-        switch (knob(GLL_KNOB_CG_GEOM)) {
-            case 1: GLL_ELLM(256, 2, 24, 1);
-            case 2: GLL_ELLM(512, 1, 24, 3);
-            case 3: GLL_ELLM(256, 2, 24, 3);
-            case 4: GLL_ELLM(256, 2, 16, 3);
-            case 5: GLL_ELLM(256, 2, 12, 3);
-            case 6: GLL_ELLM(256, 2, 12, 1);
-            case 7: GLL_ELLM(128, 4, 12, 1);
-            case 8: GLL_ELLM(512, 1, 12, 3);
-            case 9: GLL_ELLM(512, 1, 8, 1);
-            default: break;
-        }
-#undef GLL_ELLM
-    }
     if (m <= 512) GLL_ELL(256, 2, 24);
     if (m <= 1024) GLL_ELL(1024, 1, 16);
     if (m <= 2048) GLL_ELL(1024, 2, 16);

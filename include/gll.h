@@ -45,8 +45,8 @@ extern "C" {
 #define GLL_ST_SOLVE_FAILED 6  /* nonzero: the fused backward's gradient workgroups gave up
                                 * waiting for the adjoint solves (~1 s); the gradient was written
                                 * as NaN.  The Python layer raises RuntimeError on it */
-#define GLL_ST_KNN_MERGE 7     /* kNN rows whose short candidate lists may have dropped a column:
-                                * the exact merge ran instead (diagnostic count) */
+#define GLL_ST_KNN_MERGE 7     /* kNN rows with more than 64 columns at the threshold scan's
+                                * bound (ties): the full-row fallback ran (diagnostic count) */
                                /* (words 8, 9 are internal) */
 #define GLL_ST_GRID_RESCUED 10 /* whole-GPU CG solves whose grid barrier timed out (a workgroup
                                 * was not resident: other kernels held the CUs) and that one
@@ -92,7 +92,7 @@ extern "C" {
 #define GLL_KNOB_VR_RV 0      /* balanced CG: virtual rows per thread (4 / 8 / 10) */
 #define GLL_KNOB_GRID_CAP 1   /* whole-GPU CG: co-resident workgroup capacity */
 #define GLL_KNOB_GRAM_TILE 2  /* pre-split Gram: 128- or 256-row tiles */
-#define GLL_KNOB_CG_GEOM 3    /* batched per-column CG geometry variant (A/B; solve.hip) */
+#define GLL_KNOB_SEL_FORM 3   /* kNN select form: 1 latency (PG 2), 2 occupancy (knn.hip) */
 #define GLL_KNOB_COUNT 4
 int gll_set_knob(int knob, int value);
 

@@ -195,12 +195,14 @@ def test_hub_row_longer_than_lds_chunk():
     assert np.diff(rp).max() > 256
 
 
-def test_duplicate_points_and_ties():
+@pytest.mark.parametrize("k", [10, 30])
+def test_duplicate_points_and_ties(k):
     """Clusters of exact duplicates: more tied candidates than the re-rank margin (the threshold
-    merge takes every tie at its threshold, more than 64 ties fall back to the exact merge), and
-    zero-distance pairs drop out of the graph as sparse.find drops them (GLL.py:198)."""
+    scan takes every tie at its threshold; more than 64 ties fall back to select_fallback's
+    full-row bisection), and zero-distance pairs drop out of the graph as sparse.find drops them
+    (GLL.py:198).  k = 30: the 64-slot candidate list."""
     rng = np.random.default_rng(5)
-    n, d, base, k = 600, 40, 100, 10
+    n, d, base = 600, 40, 100
     X = rng.standard_normal((n, d)).astype(np.float32)
     X /= np.linalg.norm(X, axis=1, keepdims=True)
     X[200:230] = X[199]     # 31 copies: ties beyond K - 1 + margin
@@ -213,7 +215,7 @@ def test_duplicate_points_and_ties():
     from graphlearninglayer_amd import _lib
     g = _gpu_knn(X, k, 1.0)
     ind = g["knn_idx"].cpu().numpy()
-    assert int(g["status"][_lib.ST_KNN_MERGE].item()) > 0   # > 64 ties: the exact merge ran
+    assert int(g["status"][_lib.ST_KNN_MERGE].item()) > 0   # > 64 ties: the fallback ran
     assert O.knn_set_mismatch(X, ind, k) == []
     Uo, st = O.forward(X, Y, 0.07, 1.0, k, knn=(ind, None))
     assert O.rel_err(U, Uo) < TOL
@@ -1089,25 +1091,24 @@ def test_locality_order_changes_no_result(eps):
     np.testing.assert_array_equal(g0, g1)
 
 
-def test_batched_cg_geometry_variants_match_oracle():
-    """The batched per-column CG geometries selectable for A/B runs (GLL_KNOB_CG_GEOM: threads x
-    rows per thread, ELL slots in registers -- entries past them from the CSR through the LDS
-    overflow -- and the single-reduction or Neumann-1 recurrence) all solve the same systems:
-    every variant within 1e-5 of the automatic choice and the oracle's 1e-4 bar (GLL.py:53,93)."""
+@pytest.mark.parametrize("k,d", [(10, 256), (30, 1024)])
+def test_select_forms_agree_bitwise(k, d):
+    """The kNN select's latency form (two candidate groups in flight; single graphs of at most
+    2,048 rows) and its occupancy form (x_i staged in LDS, one group; larger graphs and batches),
+    forced through GLL_KNOB_SEL_FORM: the same kNN lists, distances and eps bitwise on one
+    3,000-row graph -- k = 30 takes the 64-slot candidate list of the stress config -- and the
+    lists are the exact float64 kNN (GLL.py:183,205)."""
     from graphlearninglayer_amd import _lib
-    from graphlearninglayer_amd.synth import seeded_gbar
-    B = 40   # B x C > 256: the batched geometry
-    Xs, Ys, c = _synth_batch("ns", B, seed0=61)
-    G = np.stack([seeded_gbar(c["batch"], 10, 800 + g) for g in range(B)])
-    U0, g0 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G)
-    ind = _gpu_knn(Xs[3], c["k"], 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
-    Uo, st = O.forward(Xs[3], Ys[3], tau=0.07, epsilon=1.0, K=c["k"], knn=(ind, None))
-    go = O.backward(st, G[3])
+    from graphlearninglayer_amd.synth import synth
+    X, _ = synth(1000, 2000, d, r=1.0, seed=71)
+    outs = []
     try:
-        for geom in range(1, 10):
-            _lib.set_knob(_lib.KNOB_CG_GEOM, geom)
-            U1, g1 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G)
-            assert O.rel_err(U1, U0) <= 1e-5 and O.rel_err(g1, g0) <= 1e-5, geom
-            assert O.rel_err(U1[3], Uo) <= TOL and O.rel_err(g1[3], go) <= TOL, geom
+        for form in (1, 2):
+            _lib.set_knob(_lib.KNOB_SEL_FORM, form)
+            g = _gpu_knn(X, k, "auto")
+            outs.append({key: g[key].cpu().numpy() for key in ("knn_idx", "knn_d2", "eps")})
     finally:
-        _lib.set_knob(_lib.KNOB_CG_GEOM, 0)
+        _lib.set_knob(_lib.KNOB_SEL_FORM, 0)
+    for key in outs[0]:
+        np.testing.assert_array_equal(outs[0][key], outs[1][key])
+    assert _exact_knn_rows(X, outs[0]["knn_idx"], k) == []

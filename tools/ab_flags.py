@@ -26,7 +26,8 @@ ap.add_argument("--configs", default="ns")
 ap.add_argument("--batch", default="1,64")
 ap.add_argument("--reps", type=int, default=50)
 ap.add_argument("--lib", default="", help="another build of libgll.so to load instead (A/B of builds)")
-ap.add_argument("--geoms", default="0", help="GLL_KNOB_CG_GEOM values to sweep (0 = automatic)")
+ap.add_argument("--knob", type=int, default=-1, help="include/gll.h GLL_KNOB_* id to sweep")
+ap.add_argument("--values", default="0", help="values of --knob to sweep (0 = automatic)")
 a = ap.parse_args()
 
 if a.lib:
@@ -48,9 +49,10 @@ for cfg in a.configs.split(","):
         Y = torch.from_numpy(np.concatenate([np.stack(Ys)] * reps)[:B]).cuda().contiguous()
         G = torch.from_numpy(np.stack([seeded_gbar(m, 10, 7 + g) for g in range(B)])).cuda()
         ref = None
-        variants = [(int(f), int(gm)) for gm in a.geoms.split(",") for f in a.flags.split(",")]
+        variants = [(int(f), int(gm)) for gm in a.values.split(",") for f in a.flags.split(",")]
         for flags, geom in variants:
-            _lib.set_knob(_lib.KNOB_CG_GEOM, geom)
+            if a.knob >= 0:
+                _lib.set_knob(a.knob, geom)
             prob = GLL.make_problem(n, c["d"], c["base"], 10, c["k"], 0.07, EPS[cfg], flags=flags)
             nb = lib.gll_workspace_bytes(ct.byref(prob))
             ws = torch.zeros(nb * B, dtype=torch.uint8, device="cuda")
@@ -90,6 +92,6 @@ for cfg in a.configs.split(","):
                 eu = np.abs(out[0] - ref[0]).max() / np.abs(ref[0]).max()
                 eg = np.abs(out[1] - ref[1]).max() / np.abs(ref[1]).max()
                 diff = f" dU={eu:.1e} dg={eg:.1e}"
-            print(f"{cfg} B={B} flags={flags} geom={geom}: wall {1e6 * wall:8.1f} us/call-batch "
+            print(f"{cfg} B={B} flags={flags} knob={geom}: wall {1e6 * wall:8.1f} us/call-batch "
                   f"({1e6 * wall / B:.2f} us/graph) iters {st[_lib.ST_FWD_ITERS]}/"
                   f"{st[_lib.ST_BWD_ITERS]} | {' '.join(per)}{diff}", flush=True)
