@@ -97,14 +97,22 @@ def launch(a) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def cg_spmvs(iters, B, m):
-    """Matrix passes (SpMVs) of one CG solve of `iters` iterations, by the solver the library
-    picks (solve.hip cg_dispatch): the register-ELL kernel with one row per thread (single
-    graphs with m <= 512, batches with m <= 256) runs the Neumann-preconditioned form, two
-    passes per iteration plus two in setup; every other per-column kernel one per iteration
-    plus the pre-step."""
-    neumann = m <= 512 and (B == 1 or m <= 256)
-    return 2 * iters + 2 if neumann else iters + 1
+def cg_spmvs(iters, B, m, n, K, C=10):
+    """Matrix passes (SpMVs) of one CG solve of `iters` iterations, by the form the library's
+    dispatch takes (solve.hip cg_dispatch, in its order): the whole-GPU CG for a single graph
+    past m = 2048 and the balanced kernel where row_build packs virtual rows
+    (gll_internal.h vr_threads: U-block rows longer than 12 entries) make one pass per
+    iteration plus the pre-step; so do the batched 2- and 4-row register-ELL geometries.  The
+    register-ELL kernel runs the Neumann-preconditioned form -- two passes per iteration plus
+    two in setup -- for every single graph and wherever a thread owns one row: m <= 256,
+    m <= 512 with at most 256 column workgroups (B x C), 512 < m <= 1024."""
+    if B == 1 and C <= 16 and m > 2048:
+        return iters + 1
+    vr_len = 1.4 * (K - 1) * m / n
+    if m <= 2048 and vr_len > 12.0 and -(-m * (vr_len / 8 + 0.5) // 512) <= 10:
+        return iters + 1
+    one_row = m <= 256 or (m <= 512 and (B == 1 or B * C <= 256)) or 512 < m <= 1024
+    return 2 * iters + 2 if (B == 1 or one_row) else iters + 1
 
 
 def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps, B=1):
@@ -119,13 +127,15 @@ def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps, B=1):
         # SURVEY §8d SpMV roofline: B_spmv per matrix pass (the matrix and one gathered
         # vector), times the passes the solve made; the call roofline prices a whole CG
         # iteration instead (cg_iteration_bytes)
-        "cg_kernel": ("hbm", 0.5 * (cg_spmvs(iters_fwd, B, m) + cg_spmvs(iters_bwd, B, m)) * b_spmv),
+        "cg_kernel": ("hbm", 0.5 * (cg_spmvs(iters_fwd, B, m, n, K) + cg_spmvs(iters_bwd, B, m, n, K))
+                      * b_spmv),
         "edge_coef_kernel": ("hbm", 16.0 * E + 8.0 * n * C),
         "grad_spmm_kernel": ("hbm", (12.0 * E + 8.0 * n * d) if auto_eps
                              else (8.0 * E + 8.0 * n * C + 8.0 * n * d)),
     }
     # the fused backward of a single small graph (adjoint CG + feature gradient, one launch)
-    u["cg_grad_fused_kernel"] = ("hbm", cg_spmvs(iters_bwd, B, m) * b_spmv + u["grad_spmm_kernel"][1])
+    u["cg_grad_fused_kernel"] = ("hbm", cg_spmvs(iters_bwd, B, m, n, K) * b_spmv
+                                 + u["grad_spmm_kernel"][1])
     return u
 
 
@@ -134,10 +144,10 @@ def cg_iteration_bytes(cfg, graph_stats, iters_fwd, iters_bwd, B=1):
     read/written once each), which this library keeps in registers and LDS -- an 'effective'
     figure, reported beside the SpMV roofline and used by the call roofline.  Matrix passes
     as the solver makes them (cg_spmvs)."""
-    m, C = cfg["batch"], 10
+    m, C, n, K = cfg["batch"], 10, cfg["n"], cfg["k"]
     _, nnz_uu = graph_stats
     b_spmv = 8 * nnz_uu + 8 * m + 8 * m * C
-    return 0.5 * sum(cg_spmvs(it, B, m) * b_spmv + it * 28 * m * C for it in (iters_fwd, iters_bwd))
+    return 0.5 * sum(cg_spmvs(it, B, m, n, K) * b_spmv + it * 28 * m * C for it in (iters_fwd, iters_bwd))
 
 
 def cg_roofline_extras(work_spmv, work_iter, avg_s, traffic):
@@ -239,14 +249,18 @@ def batched_measure(c, eps, tau, k, B, gstats, dev, rank, steps=20, warmup=5):
         step()
     torch.cuda.synchronize()
     kid = [_lib.kernel_name(q) for q in range(_lib.K_COUNT)].index("cg_kernel")
-    _lib.prof_enable(kid, 1)
+    # every launch of every kernel bracketed (a lone bracket on the CG reads long: see main())
+    for q in range(_lib.K_COUNT):
+        _lib.prof_enable(q, 1)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     ms, cnt = _lib.prof_read(kid)
-    _lib.prof_enable(kid, 0)
+    for q in range(_lib.K_COUNT):
+        _lib.prof_enable(q, 0)
+        _lib.prof_read(q)
     bound, work = units["cg_kernel"]
     avg_s = ms / cnt / 1e3
     achieved = B * work / avg_s / 1e9
@@ -490,8 +504,11 @@ def main():
                                         "launches_per_step": cnt / 10}
         dominant = max(per_kernel, key=lambda kn: per_kernel[kn]["us_per_launch"]
                        * per_kernel[kn]["launches_per_step"])
-        # inside the timed region: bracket every PROF_PERIOD-th launch of the dominant kernel
-        _lib.prof_enable(names.index(dominant), PROF_PERIOD)
+        # inside the timed region: bracket every PROF_PERIOD-th launch of every kernel (each
+        # runs once per step here, so the same steps): a kernel whose predecessor on the stream
+        # carries no event reads up to 2 us long (profiles/r04g_path_probe.txt, "cgonly")
+        for q in range(_lib.K_COUNT):
+            _lib.prof_enable(q, PROF_PERIOD)
 
     # timed region
     if world > 1:
@@ -526,7 +543,9 @@ def main():
     call_roof_s = None
     if dominant is not None:
         ms, cnt = _lib.prof_read(names.index(dominant))
-        _lib.prof_enable(names.index(dominant), 0)
+        for q in range(_lib.K_COUNT):
+            _lib.prof_enable(q, 0)
+            _lib.prof_read(q)
         g = GLL.device_graph(X.detach(), k, eps)
         rp = g["row_ptr"].cpu().numpy()
         col = g["col"].cpu().numpy()

@@ -1271,11 +1271,14 @@ __device__ __forceinline__ ACC exact_d2(const float* __restrict__ X, const float
                         part[g2] = __builtin_fma(d2, d2, part[g2]);
                         part[g2] = __builtin_fma(d3, d3, part[g2]);
                     } else {
+                        // explicit fma chain: contraction left to the compiler differed
+                        // between instantiations (packed multiplies, then adds), and with it
+                        // the last bit of d^2 between the select's two forms
                         const f32x4 df = mask4<VEC>(va[u] - vb[g2][u], k, d);
-                        part[g2] += df.x * df.x;
-                        part[g2] += df.y * df.y;
-                        part[g2] += df.z * df.z;
-                        part[g2] += df.w * df.w;
+                        part[g2] = __builtin_fmaf(df.x, df.x, part[g2]);
+                        part[g2] = __builtin_fmaf(df.y, df.y, part[g2]);
+                        part[g2] = __builtin_fmaf(df.z, df.z, part[g2]);
+                        part[g2] = __builtin_fmaf(df.w, df.w, part[g2]);
                     }
                 }
             }

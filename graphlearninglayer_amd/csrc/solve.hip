@@ -516,7 +516,7 @@ __device__ __forceinline__ void cg_ell_body(
         }
     }
     if (tid == 0) {
-        if (st_iters) atomicMax(st_iters, it);
+        if (st_iters && (sts != 0 || gxy.y == 0 || !conv)) atomicMax(st_iters, it);   // sink: see gll.h
         if (!conv && st_nonconv) atomicAdd(st_nonconv, 1);
     }
     if (fsync) {
@@ -844,7 +844,7 @@ __global__ __launch_bounds__(NT) void cg_vr_kernel(
         }
     }
     if (tid == 0) {
-        if (st_iters) atomicMax(st_iters, it);
+        if (st_iters && (sts != 0 || gxy.y == 0 || !conv)) atomicMax(st_iters, it);   // sink: see gll.h
         if (!conv && st_nonconv) atomicAdd(st_nonconv, 1);
     }
 }
@@ -935,7 +935,7 @@ __global__ __launch_bounds__(NT) void cg_lds_kernel(
         if (out32) out32[size_t(u) * C + c] = X_[u];
     }
     if (tid == 0) {
-        if (st_iters) atomicMax(st_iters, it);
+        if (st_iters && (sts != 0 || gxy.y == 0 || !conv)) atomicMax(st_iters, it);   // sink: see gll.h
         if (!conv && st_nonconv) atomicAdd(st_nonconv, 1);
     }
 }

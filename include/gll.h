@@ -110,7 +110,12 @@ typedef struct gll_problem {
     int32_t flags;    /* GLL_FLAG_* bits, 0 by default */
     int32_t* status_sink; /* optional device words (GLL_ST_NWORDS): when non-NULL the public
                            * status words accumulate there across calls (sticky; the caller
-                           * reads and clears them when it likes) instead of the workspace */
+                           * reads and clears them when it likes) instead of the workspace.
+                           * Batched calls: GLL_ST_FWD_ITERS / BWD_ITERS in a sink hold the
+                           * iterations of graph 0 and of every column that hit max_iter --
+                           * not of every column workgroup of the batch, which would all
+                           * update one word (B = 64 NS: 640 same-address atomics per CG
+                           * launch, ~4 us) */
 } gll_problem;
 
 /* Bytes of device workspace one forward+backward pair needs. */

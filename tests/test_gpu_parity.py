@@ -787,8 +787,9 @@ def _fwd_bwd_c_abi(X, Y, k, tau, eps, gbar, flags=0):
     return U.cpu().numpy(), gx.cpu().numpy()
 
 
-def _fwd_bwd_batched_c_abi(Xs, Ys, k, tau, eps, G, flags=0):
-    """gll_forward_batched + gll_backward_batched through ctypes: (U[B], grad_X[B], iterations)."""
+def _fwd_bwd_batched_c_abi(Xs, Ys, k, tau, eps, G, flags=0, ws=None):
+    """gll_forward_batched + gll_backward_batched through ctypes: (U[B], grad_X[B]).  `ws`: a
+    workspace to reuse (default: a fresh torch.empty one)."""
     import ctypes as ct
     from graphlearninglayer_amd import _lib
     GLL = _gll()
@@ -797,7 +798,9 @@ def _fwd_bwd_batched_c_abi(Xs, Ys, k, tau, eps, G, flags=0):
     prob = GLL.make_problem(n, d, base, C, k, tau, eps, flags=flags)
     lib = _lib.lib()
     wb = lib.gll_workspace_bytes(ct.byref(prob))
-    ws = torch.empty(B * wb, dtype=torch.uint8, device="cuda")
+    if ws is None:
+        ws = torch.empty(B * wb, dtype=torch.uint8, device="cuda")
+    assert ws.numel() >= B * wb
     U = torch.empty(B, n - base, C, dtype=torch.float64, device="cuda")
     gx = torch.empty(B, n, d, dtype=torch.float32, device="cuda")
     Xd = torch.from_numpy(np.ascontiguousarray(Xs)).cuda()
@@ -872,12 +875,14 @@ def test_knn_row_panels_automatic_past_the_n2_buffer():
 @pytest.mark.parametrize("cfg,B,scale", [("ns", 8, 1.0), ("ns", 8, 1e3), ("ns", 8, 1e-3),
                                            ("fullysup", 8, 1.0), ("stress", 2, 1.0)])
 def test_fp16_distance_storage_matches_fp32(cfg, B, scale):
-    """Batches on the pre-split Gram route store D2 as fp16 x 2^e (knn.hip dput; e from the
-    graph's largest |x - x_0|^2, so features scaled by 1e3 or 1e-3 stay in range; the scale word
-    is tagged per call, so a stale or uninitialised workspace -- each call here gets a fresh
-    torch.empty one -- cannot leak in) and the select widens its error bounds by the fp16 rounding.  D2 only nominates candidates and the select is exact,
-    so U and grad_X are bitwise those of fp32 storage (GLL_FLAG_D2_F32), whose batched results
-    the other batched tests hold to single calls and the oracle."""
+    """Batches on the pre-split Gram route store D2 as fp16 x 2^e (knn.hip dput): every GEMM tile
+    recomputes e itself from the graph's row norms (a max-reduction over nrm, |x - x_0|^2) and
+    stores it as a plain word -- the same value from every tile, nothing carried over from an
+    earlier call -- so features scaled by 1e3 or 1e-3 stay in range, and a workspace reused by a
+    batch of another scale (the second call below) leaks nothing in.  The select widens its error
+    bounds by the fp16 rounding.  D2 only nominates candidates and the select is exact, so U and
+    grad_X are bitwise those of fp32 storage (GLL_FLAG_D2_F32), whose batched results the other
+    batched tests hold to single calls and the oracle."""
     from graphlearninglayer_amd import _lib
     from graphlearninglayer_amd.synth import seeded_gbar
     Xs, Ys, c = _synth_batch(cfg, B, seed0=61)
@@ -888,6 +893,14 @@ def test_fp16_distance_storage_matches_fp32(cfg, B, scale):
     Uf, gf = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, eps, G, flags=_lib.FLAG_D2_F32)
     np.testing.assert_array_equal(Uh, Uf)
     np.testing.assert_array_equal(gh, gf)
+    if scale != 1.0:   # one workspace, first a batch at 1/scale of these features, then these
+        import ctypes as ct
+        prob = _gll().make_problem(Xs.shape[1], Xs.shape[2], Ys.shape[1], Ys.shape[2], c["k"], 0.07, eps)
+        ws = torch.empty(B * _lib.lib().gll_workspace_bytes(ct.byref(prob)), dtype=torch.uint8, device="cuda")
+        _fwd_bwd_batched_c_abi((Xs / scale).astype(np.float32), Ys, c["k"], 0.07, eps, G, ws=ws)
+        Ur, gr = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, eps, G, ws=ws)
+        np.testing.assert_array_equal(Ur, Uf)
+        np.testing.assert_array_equal(gr, gf)
 
 
 def test_batched_graphs_stay_independent_with_non_finite_and_large_features():

@@ -27,6 +27,7 @@ ap.add_argument("--batch", default="1,64")
 ap.add_argument("--reps", type=int, default=50)
 ap.add_argument("--lib", default="", help="another build of libgll.so to load instead (A/B of builds)")
 ap.add_argument("--knob", type=int, default=-1, help="include/gll.h GLL_KNOB_* id to sweep")
+ap.add_argument("--sink", action="store_true", help="pass a status sink (as the torch apply does)")
 ap.add_argument("--values", default="0", help="values of --knob to sweep (0 = automatic)")
 a = ap.parse_args()
 
@@ -54,6 +55,9 @@ for cfg in a.configs.split(","):
             if a.knob >= 0:
                 _lib.set_knob(a.knob, geom)
             prob = GLL.make_problem(n, c["d"], c["base"], 10, c["k"], 0.07, EPS[cfg], flags=flags)
+            if a.sink:
+                sink = torch.zeros(_lib.ST_NWORDS, dtype=torch.int32, device="cuda")
+                prob.status_sink = sink.data_ptr()
             nb = lib.gll_workspace_bytes(ct.byref(prob))
             ws = torch.zeros(nb * B, dtype=torch.uint8, device="cuda")
             U = torch.empty(B, m, 10, dtype=torch.float64, device="cuda")
@@ -83,7 +87,7 @@ for cfg in a.configs.split(","):
                 _lib.prof_enable(q, 0)
                 if cnt:
                     per.append(f"{names[q].replace('_kernel', '')}={1e3 * ms / cnt:.2f}")
-            st = ws[: 4 * _lib.ST_NWORDS].view(torch.int32).cpu().tolist()
+            st = (sink if a.sink else ws[: 4 * _lib.ST_NWORDS].view(torch.int32)).cpu().tolist()
             out = (U.cpu().numpy(), gx.cpu().numpy())
             diff = ""
             if ref is None:
