@@ -431,6 +431,7 @@ void trace_read_gridcg(unsigned long long*);
 void trace_reset_gridcg();
 void trace_read_wg_knn(unsigned long long*);
 void trace_read_wg_solve(unsigned long long*);
+void trace_read_wg_gridcg(unsigned long long*);
 void trace_reset_knn();
 void trace_reset_rows();
 void trace_reset_solve();
@@ -454,6 +455,7 @@ extern "C" int gll_trace_read_wg(int unit, unsigned long long* out) {
     switch (unit) {
         case 0: gll::trace_read_wg_knn(out); return GLL_OK;
         case 2: gll::trace_read_wg_solve(out); return GLL_OK;
+        case 4: gll::trace_read_wg_gridcg(out); return GLL_OK;
         default: return GLL_ERR_INVALID_ARG;
     }
 }

@@ -169,6 +169,10 @@ inline int panel_rows(int n, int flags) {
 }
 
 size_t grid_cg_workspace_floats(int m, int C);
+// The whole-GPU CG's sync words at the start of its region (gridcg.hip kSyncWords): row_build
+// zeroes them before a forward whose solves take that kernel (grid_cg_route), and each solve
+// leaves them zero, so its launch needs no memset.
+constexpr int kGridSyncWords = 640;
 struct Layout;
 int ell_emit(const Layout& L, int B);
 
@@ -573,6 +577,12 @@ inline bool locality_order(const Layout& L, const Batch& bt) {
            size_t(L.n) * L.d * 4 > (size_t(4) << 20) && !(L.flags & GLL_FLAG_ROW_ORDER_OFF);
 }
 hipError_t launch_order(const Layout& L, void* ws, hipStream_t s);
+// The Luu solves of this problem try the whole-GPU CG first (solve.hip cg_dispatch): single
+// graphs past the per-column kernels' sweet spot (m > 2048), or forced by GLL_FLAG_CG_GRID.
+inline bool grid_cg_route(const Layout& L, const Batch& bt) {
+    return bt.B == 1 && L.C <= 16 && !(L.flags & GLL_FLAG_CG_PERCOL) &&
+           (L.m > 2048 || (L.flags & GLL_FLAG_CG_GRID));
+}
 hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,
                            int y_dtype, float tau, float eps_fixed, hipStream_t s);
 // b: right-hand sides of graph 0, `b_stride` bytes apart (the workspace rhs or gbar)

@@ -88,6 +88,7 @@ struct GridCgArgs {
     int32_t* st_failed;      // public GLL_ST_SOLVE_FAILED word
     int32_t* st_rescued;     // public GLL_ST_GRID_RESCUED word
     float* rescue;           // 5 m floats: the rescue solve's vectors
+    int sync_zeroed;         // pipelined kernel: the sync words are known zero (no memset)
 };
 
 // Hand-off discipline (cdna_hip_programming.md Guideline 16 R1; MI355X_MICROARCH.md
@@ -545,8 +546,12 @@ __global__ __launch_bounds__(kGT) void cg_grid_classic_kernel(Mat A, GridCgArgs 
 // ---------------------------------------------------------------------------------------
 constexpr int kMaxG = 256;            // workgroups of one pipelined solve (<= one per CU)
 constexpr int kGvMaxRows = 512;       // rows per workgroup: NG x RPG <= 64 x 8
-constexpr int kSyncLine = 32;         // words per sync counter (one 128-B line each)
-constexpr int kSyncWords = 11 * kSyncLine;   // 8 group counters, top counter, failure, rescue
+constexpr int kSyncLine = 32;         // words per sync word (one 128-B line each)
+// sync lines: [0, 8) group arrival counters, 8 top counter, 9 failure, 10 rescue, [11, 19)
+// release words (one per group), 19 exit counter
+constexpr int kSyncTop = 8, kSyncFail = 9, kSyncRescue = 10, kSyncRel = 11, kSyncExit = 19;
+constexpr int kSyncWords = 20 * kSyncLine;
+static_assert(kSyncWords == kGridSyncWords, "gll_internal.h kGridSyncWords (row_build zeroes them)");
 
 struct GvArgs {
     int m, C, Cp, NQ, PW, max_iter;   // PW: partial floats per workgroup (32 or 64)
@@ -557,7 +562,7 @@ struct GvArgs {
     float* out32;                     // m x C results (optional)
     float* V;                         // [2][m][Cp] published vectors (u0, then m_i), by parity
     float* part;                      // [2][kMaxG][PW] partial sums, by parity
-    unsigned* sync;                   // kSyncWords, zeroed before the launch
+    unsigned* sync;                   // kSyncWords: zero at launch (gv_exit leaves them so)
     int rows_per_wg;
     int lds_cap;                      // matrix entries the dynamic LDS slice holds
     int hier;                         // two-level barrier (8 counters, then one)
@@ -569,39 +574,49 @@ struct GvArgs {
     float* rescue;                    // 5 m floats: the rescue solve's vectors
 };
 
-// Grid barrier of the pipelined kernel.  Every wave drains its sc1 stores (asm vmcnt(0):
-// MI355X_MICROARCH.md's compiler hazard), the workgroup meets, and lane 0 arrives:
-//  - flat: a relaxed agent-scope add to the top counter (G arrivals per epoch);
-//  - hier: an add to counter (block % 8) whose returned value tells the group's last
-//    arriver, which alone adds to the top counter (8 arrivals per epoch).
-// Placement-independent either way (the groups are block-index classes, not XCDs; they only
-// coincide with XCDs for speed).  Lane 0 then polls the top counter with sc1 loads and
-// s_sleep; the spin is bounded and a timeout raises the failure word everyone else also
-// watches.  Monotonic counters: epoch e waits for e x arrivals.
+// Grid barrier of the pipelined kernel.  Every wave drains its sc1 stores (asm vmcnt(0): the
+// compiler does not count the buffer stores' completion by itself), the workgroup meets, and
+// thread 0 arrives (relaxed agent-scope atomics, performed at the memory side):
+//  - hier: an add to arrival counter (block % 8) whose returned value tells the group's last
+//    arriver, which alone adds to the top counter (8 arrivals per epoch);
+//  - flat: an add to the top counter (G arrivals per epoch).
+// The arrival that completes the top counter writes the epoch into the 8 release words, and
+// every workgroup polls its group's release word (sc1 loads, s_sleep): no poller reads a line
+// that atomics land on -- round 3 polled the top counter itself, 256 pollers on the line the
+// last arrivals were adding to, and the release came ~2.2 us after the last arrival
+// (profiles/r04j_gv_trace.txt).  Placement-independent (the groups are block-index classes;
+// they coincide with XCDs only for speed).  The spin is bounded and a timeout raises the
+// failure word every poller also watches.  Monotonic: epoch e waits for e x arrivals.
 __device__ __forceinline__ bool gv_barrier(unsigned* sync, unsigned epoch, int G, int hier,
                                            int* s_ok) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned* top = sync + 8 * kSyncLine;
-        unsigned* fail = sync + 9 * kSyncLine;
-        unsigned target;
+        unsigned* top = sync + kSyncTop * kSyncLine;
+        unsigned* fail = sync + kSyncFail * kSyncLine;
+        unsigned* rel = sync + kSyncRel * kSyncLine;
+        const int ng = G < 8 ? G : 8;
+        const int g = int(blockIdx.x) % ng;
+        bool last;
         if (hier) {
-            const int ng = G < 8 ? G : 8;
-            const int g = int(blockIdx.x) % ng;
             const unsigned gs = unsigned((G - g + ng - 1) / ng);
             const unsigned old = __hip_atomic_fetch_add(sync + g * kSyncLine, 1u, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT);
-            if (old + 1u == epoch * gs)
-                __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            target = epoch * unsigned(ng);
+            last = old + 1u == epoch * gs &&
+                   __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u ==
+                       epoch * unsigned(ng);
         } else {
-            __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            target = epoch * unsigned(G);
+            last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u ==
+                   epoch * unsigned(G);
         }
+        if (last)
+            for (int q = 0; q < ng; ++q)
+                __hip_atomic_store(rel + q * kSyncLine, epoch, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         int ok = 1;
         unsigned spins = 0;
-        while (__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        while (__hip_atomic_load(rel + g * kSyncLine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+               epoch) {
             __builtin_amdgcn_s_sleep(1);
             if ((++spins & 1023u) == 0) {
                 if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -620,6 +635,21 @@ __device__ __forceinline__ bool gv_barrier(unsigned* sync, unsigned epoch, int G
     }
     __syncthreads();
     return *s_ok != 0;
+}
+
+// End of a pipelined solve: every workgroup counts out, and the last one returns the sync words
+// to zero (every other workgroup of the grid has left, rescued or not), so the next solve on
+// this workspace starts from zero without a memset launch (row_build zeroes them before a
+// forward; gll_cg_csr's caller workspace still gets a memset).
+__device__ __forceinline__ void gv_exit(unsigned* sync, int G, int* s_flag) {
+    __syncthreads();
+    if (threadIdx.x == 0)
+        *s_flag = __hip_atomic_fetch_add(sync + kSyncExit * kSyncLine, 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) == unsigned(G - 1);
+    __syncthreads();
+    if (*s_flag)
+        for (int t = threadIdx.x; t < kSyncWords; t += blockDim.x)
+            __hip_atomic_store(sync + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Sum over each aligned group of LPR lanes, result in every lane of the group (DPP: quad
@@ -662,10 +692,7 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
     __shared__ int s_len[kGvMaxRows];
     __shared__ float s_wp[NT / kWave][64];        // per-wave partials, slots [0,3C)
     __shared__ f32x4 s_red[NT / kWave][16];       // per-wave sums of the loaded partials
-    __shared__ float s_tot[64];
-    __shared__ float s_alpha[kGCM], s_beta[kGCM], s_gold[kGCM], s_aold[kGCM], s_tol2[kGCM];
-    __shared__ int s_act[kGCM];
-    __shared__ int s_any, s_ok;
+    __shared__ int s_ok;
     constexpr int NG = NT / LPR;
     constexpr int NW = NT / kWave;
     constexpr int JP = kMaxG * 16 / NT;   // partial float4 loads per thread
@@ -797,12 +824,10 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
             }
         }
     }
-    if (threadIdx.x < kGCM) {
-        s_act[threadIdx.x] = threadIdx.x < C ? 1 : 0;
-        s_alpha[threadIdx.x] = s_beta[threadIdx.x] = 0.f;
-        s_gold[threadIdx.x] = s_aold[threadIdx.x] = 1.f;
-        s_tol2[threadIdx.x] = 0.f;
-    }
+    // per-column step-size state, lane c of EVERY wave for column c (the waves compute it
+    // redundantly from the same sums in the same order: identical everywhere, no broadcast)
+    int act_c = lane < C ? 1 : 0;   // 1 active, 0 converged, 2 broken down
+    float gold_c = 1.f, aold_c = 1.f, tol2_c = 0.f;
     unsigned epoch = 0;
     bool ok = gv_barrier(a.sync, ++epoch, G, a.hier, &s_ok);
     if constexpr (MODE == 0) {
@@ -818,7 +843,26 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
 
     int it = 0;
     GLL_TRACE_PT(8);
+    // trace build: block 0's checkpoints of iteration 3 (words 11-18; tools/gv_trace.py)
+#ifdef GLL_TRACE
+    // ... and every workgroup's arrival at / release from iteration 3's barrier (g_wg[0, 8192))
+#define GLL_GV_WG(slot)                                                                     \
+    do {                                                                                    \
+        if (it == 3 && threadIdx.x == 0 && blockIdx.x < 4096)                               \
+            g_wg[(slot) * 4096 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();            \
+    } while (0)
+#else
+#define GLL_GV_WG(slot) do {} while (0)
+#endif
+#define GLL_GV_PT(i)                                 \
+    do {                                             \
+        if (it == 3) GLL_TRACE_PT(i);                \
+        if (it == 4 && (i) == 11) GLL_TRACE_PT(18);  \
+        if ((i) == 12) GLL_GV_WG(0);                 \
+        if ((i) == 13) GLL_GV_WG(1);                 \
+    } while (0)
     while (ok) {
+        GLL_GV_PT(11);
         const int pub = (it + 1) & 1;
         const __amdgpu_buffer_rsrc_t rvp = pub ? rv1 : rv0;
         const __amdgpu_buffer_rsrc_t rpp = pub ? rpt1 : rpt0;
@@ -878,7 +922,9 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
                                                        0, kSc1);
             }
         }
+        GLL_GV_PT(12);
         ok = gv_barrier(a.sync, ++epoch, G, a.hier, &s_ok);
+        GLL_GV_PT(13);
         if (a.diag_fail && it == 2) ok = false;   // injected failure (uniform over the grid)
         if (!ok) break;
         if (it == 0) GLL_TRACE_PT(9);
@@ -899,6 +945,7 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
                 nn[k] = Mat::kSeparateDiag ? dg[k] * (mi[k] * w[k]) + o : o;
             }
         }
+        GLL_GV_PT(14);
         // slot q = threadIdx % NQP: fixed order over j, then lanes, then waves
         {
             f32x4 v = pl[0];
@@ -910,54 +957,56 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
             }
             if (lane < NQP) s_red[wv][lane] = v;
             __syncthreads();
-            if (threadIdx.x < NQP) {
-                f32x4 t4 = s_red[0][threadIdx.x];
-#pragma unroll
-                for (int w_ = 1; w_ < NW; ++w_) t4 += s_red[w_][threadIdx.x];
-#pragma unroll
-                for (int t = 0; t < 4; ++t) s_tot[4 * threadIdx.x + t] = t4[t];
-            }
-            __syncthreads();
         }
-        // ---- step sizes (one lane per column, identical in every workgroup)
-        if (threadIdx.x < kWave) {
-            const int c = threadIdx.x;
-            int act = 0;
+        GLL_GV_PT(15);
+        // ---- step sizes: lane c of every wave for column c, from the waves' sums added in
+        //      wave order (round 3 had one wave compute them and broadcast through LDS: two
+        //      more workgroup barriers per iteration)
+        float al_c = 0.f, be_c = 0.f;
+        bool any;
+        {
+            const int c = lane;
             if (c < C) {
-                const float gam = s_tot[c], del = s_tot[C + c], rho = s_tot[2 * C + c];
+                const float* q0 = reinterpret_cast<const float*>(&s_red[0][0]);
+                float gam = q0[c], del = q0[C + c], rho = q0[2 * C + c];
+#pragma unroll
+                for (int w_ = 1; w_ < NW; ++w_) {
+                    const float* q = reinterpret_cast<const float*>(&s_red[w_][0]);
+                    gam += q[c];
+                    del += q[C + c];
+                    rho += q[2 * C + c];
+                }
                 if (it == 0) {
                     const float tl = fmaxf(a.atol, a.rtol * sqrtf(rho));
-                    s_tol2[c] = tl * tl;
+                    tol2_c = tl * tl;
                 }
-                act = s_act[c];
-                if (act == 1 && rho <= s_tol2[c]) act = 0;   // converged
-                float al = 0.f, be = 0.f;
-                if (act == 1) {
-                    float den = del;
+                if (act_c == 1 && rho <= tol2_c) act_c = 0;   // converged
+                if (act_c == 1) {
+                    float den = del, be = 0.f;
                     if (it > 0) {
-                        be = gam / s_gold[c];
-                        den = del - be * gam / s_aold[c];
+                        be = gam / gold_c;
+                        den = del - be * gam / aold_c;
                     }
                     if (!(den > 0.f) || !(gam > 0.f)) {
-                        act = 2;   // breakdown / NaN: stops, not converged
-                        be = 0.f;
+                        act_c = 2;   // breakdown / NaN: stops, not converged
                     } else {
-                        al = gam / den;
-                        s_gold[c] = gam;
-                        s_aold[c] = al;
+                        al_c = gam / den;
+                        be_c = be;
+                        gold_c = gam;
+                        aold_c = al_c;
                     }
                 }
-                s_act[c] = act;
-                s_alpha[c] = act == 1 ? al : 0.f;
-                s_beta[c] = act == 1 ? be : 0.f;
             }
-            const unsigned long long any = __ballot(c < C && act == 1);
-            if (c == 0) s_any = (any != 0ull && it < a.max_iter) ? 1 : 0;
+            any = __ballot(c < C && act_c == 1) != 0ull && it < a.max_iter;
         }
-        __syncthreads();
-        if (!s_any) break;
-        const f32x4 al = quad_of(s_alpha, li < kGCM / 4 ? li : 0);
-        const f32x4 be = quad_of(s_beta, li < kGCM / 4 ? li : 0);
+        GLL_GV_PT(16);
+        if (!any) break;
+        f32x4 al, be;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            al[t] = __shfl(al_c, (4 * li + t) & (kWave - 1));
+            be[t] = __shfl(be_c, (4 * li + t) & (kWave - 1));
+        }
         if constexpr (MODE == 0) {   // ---- local updates (Ghysels-Vanroose recurrences)
 #pragma unroll
             for (int k = 0; k < RPG; ++k) {
@@ -987,32 +1036,36 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
             }
             ok = gv_barrier(a.sync, ++epoch, G, a.hier, &s_ok);
         }
+        GLL_GV_PT(17);
         ++it;
     }
+#undef GLL_GV_PT
+#undef GLL_GV_WG
     GLL_TRACE_PT(10);
     // a failed grid barrier (a workgroup never arrived within ~1 s): one workgroup solves the
     // system alone (rescue_solve), the others write nothing
-    if (rescued<Mat, NT>(ok, a.sync + 10 * kSyncLine, A, a, a.rescue, &s_ok)) return;
+    if (!rescued<Mat, NT>(ok, a.sync + kSyncRescue * kSyncLine, A, a, a.rescue, &s_ok)) {
 #pragma unroll
-    for (int k = 0; k < RPG; ++k) {
-        const int uu = r0 + grp + k * NG;
-        if (uu >= r1 || !qown) continue;
+        for (int k = 0; k < RPG; ++k) {
+            const int uu = r0 + grp + k * NG;
+            if (uu >= r1 || !qown) continue;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int c = 4 * li + t;
-            if (c < C) {
-                const size_t i = size_t(uu) * C + c;
-                if (a.out64) a.out64[i] = double(x[k][t]);
-                if (a.out32) a.out32[i] = x[k][t];
+            for (int t = 0; t < 4; ++t) {
+                const int c = 4 * li + t;
+                if (c < C) {
+                    const size_t i = size_t(uu) * C + c;
+                    if (a.out64) a.out64[i] = double(x[k][t]);
+                    if (a.out32) a.out32[i] = x[k][t];
+                }
             }
         }
+        const int nonconv = __popcll(__ballot(lane < C && act_c != 0));
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (a.st_iters) atomicMax(a.st_iters, it);
+            if (a.st_nonconv && nonconv) atomicAdd(a.st_nonconv, nonconv);
+        }
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        int nonconv = 0;
-        for (int c = 0; c < C; ++c) nonconv += s_act[c] != 0 ? 1 : 0;
-        if (a.st_iters) atomicMax(a.st_iters, it);
-        if (a.st_nonconv && nonconv) atomicAdd(a.st_nonconv, nonconv);
-    }
+    gv_exit(a.sync, G, &s_ok);
 }
 
 size_t grid_cg_workspace_floats(int m, int C) {
@@ -1119,7 +1172,8 @@ static hipError_t dispatch_classic(const Mat& A, const GridCgArgs& a, int64_t nn
 
 // ---- pipelined kernel
 template <class Mat, int NT, int LPR, int RPG, int MODE>
-static hipError_t launch_gv(const Mat& A, GvArgs a, int G, int64_t nnz, float* ws, hipStream_t s) {
+static hipError_t launch_gv(const Mat& A, GvArgs a, int G, int64_t nnz, float* ws, bool zeroed,
+                            hipStream_t s) {
     a.rows_per_wg = (a.m + G - 1) / G;
     G = (a.m + a.rows_per_wg - 1) / a.rows_per_wg;
     auto fn = cg_gv_kernel<Mat, NT, LPR, RPG, MODE>;
@@ -1136,12 +1190,14 @@ static hipError_t launch_gv(const Mat& A, GvArgs a, int G, int64_t nnz, float* w
     const int nb = occupancy_blocks(reinterpret_cast<const void*>(fn), NT, lds);
     if (nb < 1 || G > kMaxG || G > device_cus()) return hipErrorCooperativeLaunchTooLarge;
     a.sync = reinterpret_cast<unsigned*>(ws);
-    a.V = ws + kSyncWords;                       // 1280 B in: 256-B aligned
+    a.V = ws + kSyncWords;                       // 2560 B in: 256-B aligned
     a.part = a.V + size_t(2) * a.m * a.Cp;
     a.rescue = ws + rescue_offset(a.m, a.C);
     a.lds_cap = int(lds / 8);
-    hipError_t e = hipMemsetAsync(a.sync, 0, kSyncWords * sizeof(unsigned), s);
-    if (e != hipSuccess) return e;
+    if (!zeroed) {   // a caller's workspace (gll_cg_csr); Luu solves: row_build / gv_exit
+        const hipError_t e = hipMemsetAsync(a.sync, 0, kSyncWords * sizeof(unsigned), s);
+        if (e != hipSuccess) return e;
+    }
     if (debug_log())
         fprintf(stderr, "gll: grid CG (%s) G=%d rows/wg=%d NT=%d LPR=%d RPG=%d lds=%zu hier=%d\n",
                 MODE == 0 ? "pipelined" : "Chronopoulos-Gear", G, a.rows_per_wg, NT, LPR, RPG, lds,
@@ -1183,16 +1239,16 @@ static hipError_t dispatch_gv(const Mat& A, const GridCgArgs& c, int64_t nnz, fl
     // (16 waves: more gathers in flight per CU) for long row blocks
     const int nt = R <= 64 ? 256 : 1024;
     if (nt == 256) {
-        if (R <= 16) return launch_gv<Mat, 256, 16, 1, MODE>(A, a, G, nnz, ws, s);
-        if (R <= 32) return launch_gv<Mat, 256, 8, 1, MODE>(A, a, G, nnz, ws, s);
-        if (R <= 64) return launch_gv<Mat, 256, 4, 1, MODE>(A, a, G, nnz, ws, s);
-        if (R <= 128) return launch_gv<Mat, 256, 4, 2, MODE>(A, a, G, nnz, ws, s);
-        if (R <= 256) return launch_gv<Mat, 256, 4, 4, MODE>(A, a, G, nnz, ws, s);
+        if (R <= 16) return launch_gv<Mat, 256, 16, 1, MODE>(A, a, G, nnz, ws, c.sync_zeroed != 0, s);
+        if (R <= 32) return launch_gv<Mat, 256, 8, 1, MODE>(A, a, G, nnz, ws, c.sync_zeroed != 0, s);
+        if (R <= 64) return launch_gv<Mat, 256, 4, 1, MODE>(A, a, G, nnz, ws, c.sync_zeroed != 0, s);
+        if (R <= 128) return launch_gv<Mat, 256, 4, 2, MODE>(A, a, G, nnz, ws, c.sync_zeroed != 0, s);
+        if (R <= 256) return launch_gv<Mat, 256, 4, 4, MODE>(A, a, G, nnz, ws, c.sync_zeroed != 0, s);
     } else {
-        if (R <= 64) return launch_gv<Mat, 1024, 16, 1, MODE>(A, a, G, nnz, ws, s);
-        if (R <= 128) return launch_gv<Mat, 1024, 8, 1, MODE>(A, a, G, nnz, ws, s);
-        if (R <= 256) return launch_gv<Mat, 1024, 4, 1, MODE>(A, a, G, nnz, ws, s);
-        if (R <= 512) return launch_gv<Mat, 1024, 4, 2, MODE>(A, a, G, nnz, ws, s);
+        if (R <= 64) return launch_gv<Mat, 1024, 16, 1, MODE>(A, a, G, nnz, ws, c.sync_zeroed != 0, s);
+        if (R <= 128) return launch_gv<Mat, 1024, 8, 1, MODE>(A, a, G, nnz, ws, c.sync_zeroed != 0, s);
+        if (R <= 256) return launch_gv<Mat, 1024, 4, 1, MODE>(A, a, G, nnz, ws, c.sync_zeroed != 0, s);
+        if (R <= 512) return launch_gv<Mat, 1024, 4, 2, MODE>(A, a, G, nnz, ws, c.sync_zeroed != 0, s);
     }
     return hipErrorNotSupported;
 }
@@ -1237,6 +1293,7 @@ hipError_t launch_cg_grid_luu(const Layout& L, void* wsp, const void* b, int b_d
     // the public words are one array (include/gll.h): GLL_ST_GRID_RESCUED beside SOLVE_FAILED
     a.st_rescued = st_failed ? st_failed - GLL_ST_SOLVE_FAILED + GLL_ST_GRID_RESCUED : nullptr;
     a.diag_fail = (L.flags & GLL_FLAG_DIAG_GRID_FAIL) ? 1 : 0;
+    a.sync_zeroed = 1;   // row_build zeroed them before the forward; every solve leaves them so
     // U-block entries per row ~ 1.5 (K-1) m / n on kNN graphs (union rows, U share)
     const int64_t nnz_est = int64_t(double(L.m) * (L.K - 1) * 1.5 * double(L.m) / double(L.n)) + L.m;
     return dispatch_grid(A, a, nnz_est, L.at<float>(wsp, L.cgv),

@@ -55,6 +55,7 @@ struct RowArgs {
     char* vr;           // [m][VRM] packed virtual rows of the balanced CG (VRM = 0: none)
     int VRM;
     unsigned* fsync;    // fused backward counters (solve.hip cg_grad_fused_kernel): zeroed here
+    unsigned* gsync;    // whole-GPU CG sync words (gridcg.hip), zeroed here; null: not used
     size_t wss;   // batched launches: workspace stride between graphs (bytes)
 
     template <bool FLAT>
@@ -326,6 +327,8 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
         a.fsync[32] = 0u;
         a.fsync[64] = 0u;   // a poisoned workspace (lost solve) is rebuilt here
     }
+    if (i == 0 && a.gsync)   // single graphs only (grid_cg_route)
+        for (int t = lane; t < kGridSyncWords; t += kWave) a.gsync[t] = 0u;
     const int Km1 = a.K - 1;
     int fi = -1;
     float fd = 0.f;
@@ -399,6 +402,7 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     a.vr = L.at<char>(ws, L.vr);
     a.VRM = L.VRM;
     a.fsync = L.at<unsigned>(ws, L.fsync);
+    a.gsync = grid_cg_route(L, bt) ? L.at<unsigned>(ws, L.cgv) : nullptr;
     a.wss = bt.ws;
     dim3 grid((L.n + 3) / 4, bt.B);
     prof_begin(GLL_K_FINALIZE, s);

@@ -1281,8 +1281,7 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     // (m 4096, K 30): 209 us against 288 us per solve, while at the FullySup shape (m 1250,
     // K 25) the per-column kernel with 16 slots and the LDS overflow wins.  Batches keep the
     // per-column kernels (B x C workgroups already fill the GPU).
-    if (bt.B == 1 && L.C <= 16 && !(L.flags & GLL_FLAG_CG_PERCOL) &&
-        (m > 2048 || (L.flags & GLL_FLAG_CG_GRID))) {
+    if (grid_cg_route(L, bt)) {
         const int b_dtype = sizeof(TB) == 8 ? GLL_DT_F64 : GLL_DT_F32;
         const hipError_t e = launch_cg_grid_luu(L, ws, b, b_dtype, out64, out32, rtol, 0.f,
                                                 max_iter, st_nonconv, st_iters, st_failed, s);

@@ -1,0 +1,3 @@
+# round-4 GPU session i: bench (headline + batched + auto-eps extra) and the profile set
+cd "$GRAFT_REPO_ROOT"
+bash tools/gpu_steps.sh "r04i_bench:400:python3 bench.py > gpurun_out/r04i_bench.json" || [ $? -lt 124 ] && bash tools/r04_prof.sh r04i
