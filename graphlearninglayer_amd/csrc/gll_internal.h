@@ -438,7 +438,7 @@ struct Batch {
 };
 
 // XCD-aware block numbering of batched launches.  Blocks are dealt round-robin over the 8 XCDs
-// in dispatch order (linear index L = y * gridDim.x + x, XCD = L % 8; MI355X_MICROARCH.md: a
+// in dispatch order (linear index L = y * gridDim.x + x, XCD = L % 8; DESIGN.md §3.5: a
 // speed assumption, never a correctness one).  For gridDim.y = B > 1 graphs, block (x, y) is
 // renumbered so that each XCD works through a contiguous run of the graph-major sequence: a
 // graph's blocks share one XCD's L2 (its X rows, its D2, its CSR) instead of each of the 8

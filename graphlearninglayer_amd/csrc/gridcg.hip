@@ -13,9 +13,10 @@
 // LDS once per solve, so an iteration reads nothing from global memory but the one published
 // vector and the partials.  Rows past the LDS capacity read their entries from the CSR.
 //
-// cg_grid_classic_kernel (round 1-2; GLL_GRID_CLASSIC=1 for A/B): classic two-reduction PCG,
-// two grid barriers per iteration, matrix entries and two vectors (z, p) gathered from global
-// memory every iteration.
+// cg_grid_classic_kernel (rounds 1-2): classic two-reduction PCG, two grid barriers per
+// iteration, matrix entries and two vectors (z, p) gathered from global memory every iteration;
+// kept for systems past the pipelined kernel's 512 rows per workgroup (m > 131,072) and the
+// oversubscription test.  Cross-workgroup hand-offs in both: DESIGN.md §3.5.
 //
 // Dot products: each workgroup writes its partial sums, and after the barrier EVERY
 // workgroup adds all partials in the same fixed order -- so every workgroup derives
@@ -91,11 +92,12 @@ struct GridCgArgs {
     int sync_zeroed;         // pipelined kernel: the sync words are known zero (no memset)
 };
 
-// Hand-off discipline (cdna_hip_programming.md Guideline 16 R1; MI355X_MICROARCH.md
-// "Valid forms", first table row): every byte another workgroup reads -- the published p / z
-// rows and the partial sums -- is stored write-through (sc1) and loaded sc1 (16-B buffer
-// accesses for the vectors), so the barrier needs neither an agent-scope release (L2
-// write-back, ~1.7 us) nor an acquire (L1 invalidate, ~1.7 us).
+// Hand-off discipline: every byte another workgroup reads -- the published
+// p / z rows and the partial sums -- is stored write-through (sc1) and loaded sc1 (16-B buffer
+// accesses for the vectors), so the barrier needs neither an agent-scope release (a whole-L2
+// write-back) nor an acquire (an L1/L2 invalidate); the writer drains its stores (vmcnt(0))
+// before its relaxed arrival, the reader's loads are issued after its poll has seen the
+// release.
 __device__ __forceinline__ void st_shared(float* p, float v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1096,12 +1098,12 @@ static size_t rescue_offset(int m, int C) {
     return ((classic > gv ? classic : gv) + 63) & ~size_t(63);
 }
 
-// An ordinary launch sized within the co-resident capacity.  MI355X_MICROARCH.md's price list
-// puts hipLaunchCooperativeKernel at +15-19 us of host time per launch for no residency the
-// ordinary launch lacks (its check even accepts one workgroup per CU more than the hardware
-// admits at some SGPR counts), and under rocprofv3 a process that made one crashed at exit
-// (DESIGN.md §3.2); the cooperative variant was removed in round 4.  The bounded barrier turns
-// a residency failure into GLL_ST_SOLVE_FAILED instead of a hang.
+// An ordinary launch sized within the co-resident capacity (one workgroup per CU at most, by
+// its LDS slice).  hipLaunchCooperativeKernel cost more host time per launch for no residency
+// the ordinary launch lacks, and under rocprofv3 a process that made one crashed at exit
+// (DESIGN.md §3.2); the cooperative variant was removed in round 4.  A lost barrier (a
+// workgroup kept off the GPU by other kernels) is rescued: one workgroup solves alone
+// (rescue_solve, GLL_ST_GRID_RESCUED).
 template <typename F, typename... Args>
 static hipError_t launch_persistent(F fn, int G, int nt, size_t lds, hipStream_t s,
                                     const char* what, Args... args) {

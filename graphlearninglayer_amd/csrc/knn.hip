@@ -57,7 +57,7 @@ GLL_TRACE_UNIT(knn)
 //   - the 4 feature-quarter partials of each quadrant are summed in LDS in a fixed order.
 // --------------------------------------------------------------------------------------
 // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs (block b runs on XCD
-// b % 8, MI355X_MICROARCH.md), so block b takes tile (b % 8) * ceil-share + b / 8: each XCD
+// b % 8), so block b takes tile (b % 8) * ceil-share + b / 8: each XCD
 // works through a contiguous run of the row-major upper-triangle tile list -- a band of row
 // blocks bi whose rows stay in that XCD's L2 -- instead of every XCD touching every row.
 // (Measured neutral at NS, B = 64 and stress, tools/ab_flags.py: the tile loads are bound by
@@ -731,16 +731,32 @@ __device__ __forceinline__ void supertile_tile(int t, int T, int& bi, int& bj) {
 
 // One-dimensional grid over B graphs x T (T + 1) / 2 tiles: xcd_tile deals each XCD a
 // contiguous run of the graph-major sequence, so a batch's graphs are XCD-local too.
+// t0 >= 0 (the tail of a 256-tile launch, launch_gram): block 4 j + s computes 128-subtile s of
+// 256-tile t0 + j in gram_pk2_kernel's sequence (T2 = ceil(T / 2) blocks a side); subtiles below
+// a diagonal 256-tile's diagonal or past n return at once.
 template <bool H>
 __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__ Ph,
                                                       const __bf16* __restrict__ Pl,
                                                       const float* __restrict__ nrm, int n,
                                                       int dp, int T, float* __restrict__ D2,
                                                       int ld, size_t wss,
-                                                      float* __restrict__ d2s) {
-    const int NT = T * (T + 1) / 2;
-    const int idx = xcd_tile(blockIdx.x, gridDim.x);
-    const int g = idx / NT;
+                                                      float* __restrict__ d2s, int t0) {
+    int g, bi, bj;
+    if (t0 < 0) {
+        const int NT = T * (T + 1) / 2;
+        const int idx = xcd_tile(blockIdx.x, gridDim.x);
+        g = idx / NT;
+        supertile_tile(idx - g * NT, T, bi, bj);
+    } else {
+        const int T2 = (T + 1) / 2, NT2 = T2 * (T2 + 1) / 2;
+        const int idx2 = t0 + int(blockIdx.x >> 2), sub = int(blockIdx.x & 3);
+        int b2i, b2j;
+        g = idx2 / NT2;
+        supertile_tile(idx2 - g * NT2, T2, b2i, b2j);
+        bi = 2 * b2i + (sub >> 1);
+        bj = 2 * b2j + (sub & 1);
+        if (bi > bj || bj >= T) return;   // whole workgroup, before any barrier
+    }
     {
         const size_t off = size_t(g) * wss;   // graph g's workspace block
         Ph = reinterpret_cast<const __bf16*>(reinterpret_cast<const char*>(Ph) + off);
@@ -754,8 +770,6 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
-    int bi, bj;
-    supertile_tile(idx - g * NT, T, bi, bj);
     const int wr = w >> 1, wc = w & 1;
     // this lane's DMA sources: 16 per stage = plane q >> 2, rows 8 c .. 8 c + 7 (c = (q & 3) 4 + w)
     // as 1 KiB pieces; lane -> row 8 c + lane / 8, LDS segment lane % 8 <- source segment
@@ -2040,24 +2054,38 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         __bf16* Ph = L.at<__bf16>(ws, L.xhi);
         __bf16* Pl = L.at<__bf16>(ws, L.xlo);
         float* nrm = L.at<float>(ws, L.xnrm);
+        const bool H = d2_half(L, bt);
+        const int T2 = (L.n + 255) / 256;
+        const bool t256 = gram_tile256(L, bt, T, T2);
+        // one 256-tile per CU at a time: a last round short of a full one (stress: 528 tiles, 16
+        // in the third round, profiles/r04b_stress_kernel_stats.csv) runs as the 128-subtiles of
+        // those tiles instead (gram_pk_kernel's D2 is bitwise the 256-tile kernel's), when they
+        // take at most two rounds
+        const int64_t nt2 = int64_t(bt.B) * T2 * (T2 + 1) / 2;
+        const int cus = device_cus();
+        int64_t tail = t256 && nt2 > cus ? nt2 % cus : 0;
+        if (tail * 4 > int64_t(2) * cus || knob(GLL_KNOB_GRAM_TAIL) == 1) tail = 0;
         prof_begin(GLL_K_GRAM, s);
-        prof_span(2);
+        prof_span(tail > 0 ? 3 : 2);
         const dim3 sgrid((L.n + 3) / 4, bt.B);
         float* d2s = L.at<float>(ws, L.d2s);
         if (vec)
             launch_k(gram_split_kernel<true>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
         else
             launch_k(gram_split_kernel<false>, sgrid, 256, 0, s, X, L.n, L.d, L.dp, Ph, Pl, nrm, st, rc, bt.x, bt.ws);
-        const bool H = d2_half(L, bt);
-        const int T2 = (L.n + 255) / 256;
-        if (gram_tile256(L, bt, T, T2))
+        if (t256) {
             launch_k(H ? gram_pk2_kernel<true> : gram_pk2_kernel<false>,
-                     dim3(unsigned(bt.B * T2 * (T2 + 1) / 2)), 512, 0, s, Ph, Pl, nrm, L.n, L.dp,
-                     T2, D2, L.ldD, bt.ws, d2s);
-        else
+                     dim3(unsigned(nt2 - tail)), 512, 0, s, Ph, Pl, nrm, L.n, L.dp, T2, D2,
+                     L.ldD, bt.ws, d2s);
+            if (tail > 0)
+                launch_k(H ? gram_pk_kernel<true> : gram_pk_kernel<false>,
+                         dim3(unsigned(4 * tail)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T, D2, L.ldD,
+                         bt.ws, d2s, int(nt2 - tail));
+        } else {
             launch_k(H ? gram_pk_kernel<true> : gram_pk_kernel<false>,
                      dim3(unsigned(bt.B * T * (T + 1) / 2)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T,
-                     D2, L.ldD, bt.ws, d2s);
+                     D2, L.ldD, bt.ws, d2s, -1);
+        }
         prof_end(GLL_K_GRAM, s);
         return launch_status("knn.hip:launch_gram(pk)");
     }

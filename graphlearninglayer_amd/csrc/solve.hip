@@ -197,7 +197,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int& total) 
 // The kernel body: `gxy` = (column, graph); `fsync` (the fused backward, cg_grad_fused_kernel)
 // non-null: the solution is stored write-through (sc1) and, once every wave has drained its
 // stores, thread 0 adds 1 to fsync[0] -- the feature-gradient workgroups of the same launch
-// wait for C arrivals (MI355X_MICROARCH.md 'Valid forms', first table row).
+// wait for C arrivals (the hand-off protocol of DESIGN.md §3.5).
 template <int NT, int R, int S, typename TB, int MODE>
 __device__ __forceinline__ void cg_ell_body(
     int2 gxy, unsigned* fsync,
