@@ -28,8 +28,7 @@ constexpr int kMaxKm1 = 56;      // K - 1 <= 56: the kNN rescan keeps >= 8 lanes
 constexpr int kStOvfCount = 8;   // internal status words: overflow-list length
 constexpr int kStBump = 9;       //                        bump-region cursor
 constexpr int kPiv = 64;         // pivot rows of the locality order (order_pid_kernel)
-constexpr int kStPiv = GLL_ST_NWORDS;   // [kPiv] rows per pivot, then [kPiv] scatter cursors
-constexpr int kStWords = GLL_ST_NWORDS + 2 * kPiv;   // words the Gram kernels zero per call
+constexpr int kStWords = GLL_ST_NWORDS;   // words the Gram kernels zero per call
 
 // ELL slice width of the per-column CG kernels for m unlabeled rows (solve.hip dispatch);
 // row_build emits that many column-major (col, w) slots per U row, 0 when no ELL kernel runs.
@@ -198,6 +197,7 @@ struct Layout {
                       // [64] poison (a lost solve: the counters may be stale)
     size_t d2s;       // float: the fp16 D2 scale of the pre-split GEMM (knn.hip tile_d2_scale)
     size_t pid, perm; // locality order (order_rows): nearest pivot of each row, the row order
+    size_t ohist;     // locality order: rows per pivot of each 64-row block ([ceil(n/64)][64])
 
     explicit Layout(const gll_problem& p) {
         n = p.n; d = p.d; base = p.base; C = p.C;
@@ -252,6 +252,7 @@ struct Layout {
         d2s = take(256);     // fp16 D2 scale of the pre-split Gram (knn.hip tile_d2_scale)
         pid = take(size_t(n) * 4);
         perm = take(size_t(n) * 4);
+        ohist = take(size_t((n + 63) / 64) * 64 * 4);
         P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)
         Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
         S = take(size_t(Etot) * 4);        // per-edge coefficient (auto eps / chunked gradient)

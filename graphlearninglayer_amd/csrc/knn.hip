@@ -1925,18 +1925,24 @@ __device__ __forceinline__ int pivot_row(int j, int n) {
 }
 
 // 64 rows per workgroup, the pivots split over its 4 waves (16 each: every load of a lane
-// issued together), the 4 partial minima combined in LDS in pivot order.
+// issued together), the 4 partial minima combined in LDS in pivot order.  The block's rows per
+// pivot go out as one plain 64-int histogram row: round 4 had every row atomically add to one
+// of 64 global counters, 8,192 same-address atomics at stress that made this a 13.9 us kernel
+// (profiles/r04b_stress_kernel_stats.csv).
 template <int NP>
 __global__ __launch_bounds__(256) void order_pid_kernel(const float* __restrict__ D2, int ld,
                                                         size_t plane, int n,
                                                         int32_t* __restrict__ pid,
-                                                        int32_t* __restrict__ status) {
+                                                        int32_t* __restrict__ hist) {
     constexpr int PPW = kPiv / 4;   // pivots per wave
+    static_assert(kPiv == kWave, "one histogram bin per lane");
     __shared__ float s_best[4][kWave];
     __shared__ int s_arg[4][kWave];
+    __shared__ int s_cnt[kPiv];
     const int lane = lane_id(), wv = threadIdx.x >> 6;
     const int i = int(blockIdx.x) * kWave + lane;
     const int ic = i < n ? i : n - 1;
+    if (wv == 1) s_cnt[lane] = 0;
     float v[PPW];
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {   // every load issued before any is compared
@@ -1956,31 +1962,48 @@ __global__ __launch_bounds__(256) void order_pid_kernel(const float* __restrict_
     s_best[wv][lane] = best;
     s_arg[wv][lane] = bp;
     __syncthreads();
-    if (wv == 0 && i < n) {
+    if (wv == 0) {
 #pragma unroll
         for (int w = 1; w < 4; ++w)
             if (s_best[w][lane] < best) {
                 best = s_best[w][lane];
                 bp = s_arg[w][lane];
             }
-        pid[i] = bp;
-        atomicAdd(&status[kStPiv + bp], 1);
+        if (i < n) {
+            pid[i] = bp;
+            atomicAdd(&s_cnt[bp], 1);
+        }
     }
+    __syncthreads();
+    if (wv == 1) hist[size_t(blockIdx.x) * kPiv + lane] = s_cnt[lane];
 }
 
-// One workgroup: the pivots' row counts -> offsets (wave 0's scan), then every row to its
-// pivot's range (LDS cursors; the order inside a range is arbitrary -- speed only).  Each
-// thread's pivot ids are all loaded before its first cursor atomic.
+// One workgroup: the pivots' row counts (the blocks' histograms summed) -> offsets (wave 0's
+// scan), then every row to its pivot's range (LDS cursors; the order inside a range is
+// arbitrary -- speed only).  Each thread's pivot ids are all loaded before its first cursor
+// atomic.
 __global__ __launch_bounds__(1024) void order_perm_kernel(int n, const int32_t* __restrict__ pid,
-                                                          const int32_t* __restrict__ status,
+                                                          const int32_t* __restrict__ hist,
                                                           int32_t* __restrict__ perm) {
     static_assert(kPiv == kWave, "one wave scans the pivot counts");
     constexpr int U = 8;
+    constexpr int NGRP = 1024 / kPiv;   // block groups summing one pivot's counts
+    __shared__ int part[NGRP][kPiv];
     __shared__ int base[kPiv];
     __shared__ int cur[kPiv];
     const int tid = threadIdx.x;
+    const int nb = (n + kWave - 1) / kWave;
+    {
+        const int pv = tid & (kPiv - 1), grp = tid / kPiv;
+        int c = 0;
+        for (int b = grp; b < nb; b += NGRP) c += hist[size_t(b) * kPiv + pv];
+        part[grp][pv] = c;
+    }
+    __syncthreads();
     if (tid < kWave) {
-        const int c = status[kStPiv + tid];
+        int c = 0;
+#pragma unroll
+        for (int g = 0; g < NGRP; ++g) c += part[g][tid];
         int incl = c;
 #pragma unroll
         for (int off = 1; off < kWave; off <<= 1) {
@@ -2006,16 +2029,16 @@ __global__ __launch_bounds__(1024) void order_perm_kernel(int n, const int32_t* 
 
 hipError_t launch_order(const Layout& L, void* ws, hipStream_t s) {
     const float* D2 = L.at<float>(ws, L.D2);
-    int32_t* st = L.at<int32_t>(ws, L.status);
+    int32_t* hist = L.at<int32_t>(ws, L.ohist);
     int32_t* pid = L.at<int32_t>(ws, L.pid);
     const size_t plane = size_t(L.n) * L.ldD;
     const dim3 grid(unsigned((L.n + kWave - 1) / kWave));
     if (gram_planes(L, 1) == 2)
-        launch_k(order_pid_kernel<2>, grid, 256, 0, s, D2, L.ldD, plane, L.n, pid, st);
+        launch_k(order_pid_kernel<2>, grid, 256, 0, s, D2, L.ldD, plane, L.n, pid, hist);
     else
-        launch_k(order_pid_kernel<1>, grid, 256, 0, s, D2, L.ldD, plane, L.n, pid, st);
+        launch_k(order_pid_kernel<1>, grid, 256, 0, s, D2, L.ldD, plane, L.n, pid, hist);
     launch_k(order_perm_kernel, dim3(1), 1024, 0, s, L.n, static_cast<const int32_t*>(pid),
-             static_cast<const int32_t*>(st), L.at<int32_t>(ws, L.perm));
+             static_cast<const int32_t*>(hist), L.at<int32_t>(ws, L.perm));
     return launch_status("knn.hip:launch_order");
 }
 
@@ -2060,11 +2083,11 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         // one 256-tile per CU at a time: a last round short of a full one (stress: 528 tiles, 16
         // in the third round, profiles/r04b_stress_kernel_stats.csv) runs as the 128-subtiles of
         // those tiles instead (gram_pk_kernel's D2 is bitwise the 256-tile kernel's), when they
-        // take at most two rounds
+        // fit one round (B = 64 NS: 128 tail tiles, two rounds of subtiles measured 224 -> 235 us)
         const int64_t nt2 = int64_t(bt.B) * T2 * (T2 + 1) / 2;
         const int cus = device_cus();
         int64_t tail = t256 && nt2 > cus ? nt2 % cus : 0;
-        if (tail * 4 > int64_t(2) * cus || knob(GLL_KNOB_GRAM_TAIL) == 1) tail = 0;
+        if (tail * 4 > cus || knob(GLL_KNOB_GRAM_TAIL) == 1) tail = 0;
         prof_begin(GLL_K_GRAM, s);
         prof_span(tail > 0 ? 3 : 2);
         const dim3 sgrid((L.n + 3) / 4, bt.B);

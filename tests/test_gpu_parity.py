@@ -1056,12 +1056,12 @@ def test_fused_backward_equals_two_launches_bitwise(cfg):
 
 @pytest.mark.parametrize("cfg,B,n_extra,d", [("ns", 3, 0, None), ("fullysup", 2, 0, None),
                                              ("ns", 2, 37, 100), ("ns", 26, 0, None),
-                                             ("ns", 18, 37, 100)])
+                                             ("ns", 26, 37, 100)])
 def test_gram_256_tiles_match_128_tiles(cfg, B, n_extra, d, monkeypatch):
     """The 256-tile pre-split Gram (knn.hip gram_pk2_kernel, 8 waves) against the 128-tile one
     (gram_pk_kernel) on batches, ragged n and d included: the same k order and epilogue, so U
-    and grad_X agree bitwise (the GLL_KNOB_GRAM_TILE test knob forces either).  B = 26 (n 1,000)
-    and 18 (n 1,037): 260 and 270 256-tiles on a 256-CU device, whose short last round runs as 128-subtiles (the
+    and grad_X agree bitwise (the GLL_KNOB_GRAM_TILE test knob forces either).  B = 26 (n 1,000
+    and 1,037): 260 256-tiles on a 256-CU device, whose short last round runs as 128-subtiles (the
     launch's tail)."""
     from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth
     GLL = _gll()
