@@ -758,7 +758,11 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
     // n = A v over the owned rows: lane li gathers entries li, li + LPR, ... (chunks of CH per
     // lane, every gather of a chunk in flight together), the group sums by DPP, lane li keeps
     // quad li.  Dead entries load from an out-of-range offset (the buffer returns 0).
-    constexpr int CH = NT >= 1024 ? 2 : 4;   // 16 waves: fewer gathers per lane, no spills
+    // 256 threads: a row of up to 8 LPR entries in one round of gathers (the barrier waits for
+    // the workgroup with the longest rows: at stress, 4 per lane left hub rows a second round
+    // trip, and iteration 3's arrivals spread over 1.2 us, profiles/r04l_gv_trace.txt); 16 waves:
+    // fewer gathers per lane, no spills
+    constexpr int CH = NT >= 1024 ? 2 : 8;
     auto spmv = [&](int k, __amdgpu_buffer_rsrc_t rv) -> f32x4 {
         f32x4 acc[kGCM / 4];
 #pragma unroll

@@ -1925,10 +1925,11 @@ __device__ __forceinline__ int pivot_row(int j, int n) {
 }
 
 // 64 rows per workgroup, the pivots split over its 4 waves (16 each: every load of a lane
-// issued together), the 4 partial minima combined in LDS in pivot order.  The block's rows per
-// pivot go out as one plain 64-int histogram row: round 4 had every row atomically add to one
-// of 64 global counters, 8,192 same-address atomics at stress that made this a 13.9 us kernel
-// (profiles/r04b_stress_kernel_stats.csv).
+// issued together), the 4 partial minima combined in LDS in pivot order.  Wave 0 then ranks its
+// rows within their pivot (lane order: pid = pivot | rank << 8) and writes the block's rows per
+// pivot as one plain 64-int histogram row.  (The first version counted with one global atomic
+// per row on 64 counters: 8,192 same-address atomics made this a 13.9 us kernel at stress,
+// profiles/r04b_stress_kernel_stats.csv; order_perm then scattered through LDS cursor atomics.)
 template <int NP>
 __global__ __launch_bounds__(256) void order_pid_kernel(const float* __restrict__ D2, int ld,
                                                         size_t plane, int n,
@@ -1938,11 +1939,9 @@ __global__ __launch_bounds__(256) void order_pid_kernel(const float* __restrict_
     static_assert(kPiv == kWave, "one histogram bin per lane");
     __shared__ float s_best[4][kWave];
     __shared__ int s_arg[4][kWave];
-    __shared__ int s_cnt[kPiv];
     const int lane = lane_id(), wv = threadIdx.x >> 6;
     const int i = int(blockIdx.x) * kWave + lane;
     const int ic = i < n ? i : n - 1;
-    if (wv == 1) s_cnt[lane] = 0;
     float v[PPW];
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {   // every load issued before any is compared
@@ -1962,43 +1961,45 @@ __global__ __launch_bounds__(256) void order_pid_kernel(const float* __restrict_
     s_best[wv][lane] = best;
     s_arg[wv][lane] = bp;
     __syncthreads();
-    if (wv == 0) {
+    if (wv != 0) return;
 #pragma unroll
-        for (int w = 1; w < 4; ++w)
-            if (s_best[w][lane] < best) {
-                best = s_best[w][lane];
-                bp = s_arg[w][lane];
-            }
-        if (i < n) {
-            pid[i] = bp;
-            atomicAdd(&s_cnt[bp], 1);
+    for (int w = 1; w < 4; ++w)
+        if (s_best[w][lane] < best) {
+            best = s_best[w][lane];
+            bp = s_arg[w][lane];
         }
+    const bool valid = i < n;
+    int rank = 0, cnt = 0;   // cnt: rows of this block at pivot `lane`
+    uint64_t todo = __ballot(valid);
+    while (todo) {   // one round per distinct pivot of the block (wave-uniform)
+        const int v0 = __builtin_amdgcn_readlane(bp, int(__builtin_ctzll(todo)));
+        const uint64_t mk = __ballot(valid && bp == v0);
+        if (valid && bp == v0) rank = lanes_below(mk);
+        if (lane == v0) cnt = __popcll(mk);
+        todo &= ~mk;
     }
-    __syncthreads();
-    if (wv == 1) hist[size_t(blockIdx.x) * kPiv + lane] = s_cnt[lane];
+    if (valid) pid[i] = bp | (rank << 8);
+    hist[size_t(blockIdx.x) * kPiv + lane] = cnt;
 }
 
-// One workgroup: the pivots' row counts (the blocks' histograms summed) -> offsets (wave 0's
-// scan), then every row to its pivot's range (LDS cursors; the order inside a range is
-// arbitrary -- speed only).  Each thread's pivot ids are all loaded before its first cursor
-// atomic.
+// One workgroup, no atomics: per pivot, the blocks' counts become exclusive offsets (16 block
+// groups per pivot, group totals scanned in LDS, pivots scanned by one wave), written back over
+// the histogram; then row i goes to offset[block i / 64][pivot] + its rank in the block.
 __global__ __launch_bounds__(1024) void order_perm_kernel(int n, const int32_t* __restrict__ pid,
-                                                          const int32_t* __restrict__ hist,
+                                                          int32_t* __restrict__ hist,
                                                           int32_t* __restrict__ perm) {
     static_assert(kPiv == kWave, "one wave scans the pivot counts");
-    constexpr int U = 8;
-    constexpr int NGRP = 1024 / kPiv;   // block groups summing one pivot's counts
+    constexpr int NGRP = 1024 / kPiv;   // block groups per pivot
     __shared__ int part[NGRP][kPiv];
-    __shared__ int base[kPiv];
-    __shared__ int cur[kPiv];
+    __shared__ int goff[NGRP][kPiv];
     const int tid = threadIdx.x;
     const int nb = (n + kWave - 1) / kWave;
-    {
-        const int pv = tid & (kPiv - 1), grp = tid / kPiv;
-        int c = 0;
-        for (int b = grp; b < nb; b += NGRP) c += hist[size_t(b) * kPiv + pv];
-        part[grp][pv] = c;
-    }
+    const int per = (nb + NGRP - 1) / NGRP;
+    const int pv = tid & (kPiv - 1), grp = tid / kPiv;
+    const int b0 = grp * per, b1 = min(nb, b0 + per);
+    int run = 0;
+    for (int b = b0; b < b1; ++b) run += hist[size_t(b) * kPiv + pv];
+    part[grp][pv] = run;
     __syncthreads();
     if (tid < kWave) {
         int c = 0;
@@ -2010,20 +2011,25 @@ __global__ __launch_bounds__(1024) void order_perm_kernel(int n, const int32_t* 
             const int t = __shfl_up(incl, off);
             if (tid >= off) incl += t;
         }
-        base[tid] = incl - c;
-        cur[tid] = 0;
+        int o = incl - c;
+#pragma unroll
+        for (int g = 0; g < NGRP; ++g) {
+            goff[g][tid] = o;
+            o += part[g][tid];
+        }
     }
     __syncthreads();
-    for (int i0 = 0; i0 < n; i0 += 1024 * U) {
-        int p[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = i0 + u * 1024 + tid;
-            p[u] = i < n ? pid[i] : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (p[u] >= 0) perm[base[p[u]] + atomicAdd(&cur[p[u]], 1)] = i0 + u * 1024 + tid;
+    int o = goff[grp][pv];
+    for (int b = b0; b < b1; ++b) {
+        const size_t q = size_t(b) * kPiv + pv;
+        const int h = hist[q];
+        hist[q] = o;
+        o += h;
+    }
+    __syncthreads();   // the offsets are visible to the whole workgroup
+    for (int i = tid; i < n; i += 1024) {
+        const int v = pid[i];
+        perm[hist[size_t(i >> 6) * kPiv + (v & 0xFF)] + (v >> 8)] = i;
     }
 }
 
@@ -2037,8 +2043,8 @@ hipError_t launch_order(const Layout& L, void* ws, hipStream_t s) {
         launch_k(order_pid_kernel<2>, grid, 256, 0, s, D2, L.ldD, plane, L.n, pid, hist);
     else
         launch_k(order_pid_kernel<1>, grid, 256, 0, s, D2, L.ldD, plane, L.n, pid, hist);
-    launch_k(order_perm_kernel, dim3(1), 1024, 0, s, L.n, static_cast<const int32_t*>(pid),
-             static_cast<const int32_t*>(hist), L.at<int32_t>(ws, L.perm));
+    launch_k(order_perm_kernel, dim3(1), 1024, 0, s, L.n, static_cast<const int32_t*>(pid), hist,
+             L.at<int32_t>(ws, L.perm));
     return launch_status("knn.hip:launch_order");
 }
 
