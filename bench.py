@@ -104,15 +104,15 @@ def cg_spmvs(iters, B, m, n, K, C=10):
     (gll_internal.h vr_threads: U-block rows longer than 12 entries) make one pass per
     iteration plus the pre-step; so do the batched 2- and 4-row register-ELL geometries.  The
     register-ELL kernel runs the Neumann-preconditioned form -- two passes per iteration plus
-    two in setup -- for every single graph and wherever a thread owns one row: m <= 256,
-    m <= 512 with at most 256 column workgroups (B x C), 512 < m <= 1024."""
+    two in setup -- wherever a thread owns one row: m <= 256, m <= 512 for a single graph or at
+    most 256 column workgroups (B x C), 512 < m <= 1024."""
     if B == 1 and C <= 16 and m > 2048:
         return iters + 1
     vr_len = 1.4 * (K - 1) * m / n
     if m <= 2048 and vr_len > 12.0 and -(-m * (vr_len / 8 + 0.5) // 512) <= 10:
         return iters + 1
     one_row = m <= 256 or (m <= 512 and (B == 1 or B * C <= 256)) or 512 < m <= 1024
-    return 2 * iters + 2 if (B == 1 or one_row) else iters + 1
+    return 2 * iters + 2 if one_row else iters + 1
 
 
 def kernel_units(cfg, graph_stats, iters_fwd, iters_bwd, auto_eps, B=1):

@@ -1008,8 +1008,11 @@ __device__ __forceinline__ bool select_threshold(const D2Row<H>& row, size_t pla
     constexpr int HV = CH > 0 ? CH * NB * 4 : 1;
     const int lane = lane_id();
     uint32_t m[TOP];
+    int mj[CH > 0 ? 1 : TOP];   // CH = 0: the columns of the lane's TOP smallest
 #pragma unroll
     for (int t = 0; t < TOP; ++t) m[t] = 0xFFFFFFFFu;
+#pragma unroll
+    for (int t = 0; t < (CH > 0 ? 1 : TOP); ++t) mj[t] = -1;
     uint32_t hv[HV];
     auto load_chunk = [&](int jb, f32x4 (&v)[NB]) {
 #pragma unroll
@@ -1035,6 +1038,19 @@ __device__ __forceinline__ bool select_threshold(const D2Row<H>& row, size_t pla
             m[t] = lo;
         }
     };
+    auto absorb_j = [&](uint32_t u, int j) {   // the same network carrying the column
+        nvalid += u != 0xFFFFFFFFu ? 1 : 0;
+#pragma unroll
+        for (int t = 0; t < (CH > 0 ? 1 : TOP); ++t) {
+            const bool sw = u < m[t];
+            const uint32_t mt = m[t];
+            const int jt = mj[t];
+            m[t] = sw ? u : mt;
+            mj[t] = sw ? j : jt;
+            u = sw ? mt : u;
+            j = sw ? jt : j;
+        }
+    };
     if constexpr (CH > 0) {   // the row was loaded by the caller (prefetched under the last row)
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
@@ -1054,7 +1070,10 @@ __device__ __forceinline__ bool select_threshold(const D2Row<H>& row, size_t pla
 #pragma unroll
             for (int b = 0; b < NB; ++b)
 #pragma unroll
-                for (int t = 0; t < 4; ++t) absorb(bits_of(v[b][t], jb + 4 * (b * kWave + lane) + t));
+                for (int t = 0; t < 4; ++t) {
+                    const int j = jb + 4 * (b * kWave + lane) + t;
+                    absorb_j(bits_of(v[b][t], j), j);
+                }
         }
     }
     GLL_TRACE_PT(16);
@@ -1078,7 +1097,10 @@ __device__ __forceinline__ bool select_threshold(const D2Row<H>& row, size_t pla
         }
         T = up;
     }
-    // pass 2: compact every column <= T, in column order
+    // pass 2: compact every column <= T.  CH = 0 (rows re-read from memory): when no lane may
+    // hold more columns <= T than its TOP list (a lane whose whole list is <= T while it saw
+    // more columns), the lists ARE that set and the row is not read again -- stress: the second
+    // read was 22 of a wave's 81 us (profiles/r04p_trace_stress.txt)
     int base = 0, mine = 0;
     auto emit = [&](uint32_t u, int j) {
         const bool p = u <= T;
@@ -1099,6 +1121,9 @@ __device__ __forceinline__ bool select_threshold(const D2Row<H>& row, size_t pla
 #pragma unroll
                 for (int t = 0; t < 4; ++t)
                     emit(hv[(c * NB + b) * 4 + t], c * 4 * kWave * NB + 4 * (b * kWave + lane) + t);
+    } else if (__ballot(m[TOP - 1] <= T && nvalid > TOP) == 0ull) {
+#pragma unroll
+        for (int t = 0; t < (CH > 0 ? 1 : TOP); ++t) emit(m[t], mj[t]);
     } else {
         for (int jb = 0; jb < n; jb += 4 * kWave * NB) {
             f32x4 v[NB];

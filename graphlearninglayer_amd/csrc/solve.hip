@@ -1288,11 +1288,13 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
         if (e != hipErrorNotSupported) return e;
         // no grid configuration holds it: per-column kernels below (any m)
     }
-    // the Neumann form (MODE 3) wherever a thread owns one row; batched launches with two rows
-    // per thread keep one SpMV per iteration (MODE 3 at 256 x 2 takes 220 VGPRs, two waves per
-    // SIMD instead of three: B = 64 NS CG 21.8 -> 34.2 us; profiles/r03l_cg_neumann_ab.txt).
+    // the Neumann form (MODE 3) wherever a thread owns one row; with two or more rows per thread
+    // one SpMV per iteration (MODE 3 at 256 x 2 takes 220 VGPRs, two waves per SIMD instead of
+    // three: B = 64 NS CG 21.8 -> 34.2 us, profiles/r03l_cg_neumann_ab.txt; at 1024 x 2 it
+    // spilled 144 B per lane: FullySup single graph forced onto this kernel 174 -> 135 us per
+    // solve with MODE 1, profiles/r04p_ab_ell2.txt).
 #define GLL_ELL(NT, R, S)                                                                   \
-    return (bt.B > 1 && R > 1)                                                              \
+    return (R > 1)                                                                          \
                ? run_ell<NT, R, S, TB, 1>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
                                           st_nonconv, st_iters, s)                          \
                : run_ell<NT, R, S, TB, 3>(L, bt, ws, b, bs, out64, out32, rtol, max_iter,   \
