@@ -1435,10 +1435,9 @@ __device__ __forceinline__ KnnPick knn_rescan(const D2Row<H>& row, size_t plane,
 // registers by the threshold scan.
 template <int KC, bool VEC, int NP, int PG, int NU, int XQ = 0, bool R = false, int CH = 0,
           bool H = false>
-#ifndef GLL_SEL_WAVES
-#define GLL_SEL_WAVES 6
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XQ > 0 && NU <= 8 ? GLL_SEL_WAVES : 1)))
+// Occupancy forms (x_i in LDS): NU = 8 load steps at 6 waves per SIMD (<= 80 VGPRs), NU = 4 at
+// 8 waves per SIMD (<= 64 VGPRs).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XQ > 0 ? (NU <= 4 ? 8 : (NU <= 8 ? 6 : 1)) : 1)))
 void knn_select_kernel(
     const float* __restrict__ D2, int ld, size_t plane, const float* __restrict__ X, int n, int d, int K,
     int kc, float eps_fixed, int auto_eps, int RCAP, int32_t* __restrict__ knn_idx,
@@ -1479,16 +1478,18 @@ void knn_select_kernel(
         i = r0 + gxy.x * 4 + wv;
         if (i >= r1) return;  // whole wave
     }
-    // XL: x_i is staged once in LDS (its loads ride under the D2 scan's), so the exact
-    // distances hold only the candidates' rows in registers (occupancy) and do not re-load x_i
-    // per sweep.  Features past d are zero (masked at use anyway).
-    f32x4 xr[XL ? XQ : 1];
+    // XL: x_i is staged once in LDS by LDS-DMA (global_load_lds: no registers held across the
+    // D2 scan -- round 3 staged it through 4 XQ VGPRs that stayed live until the scan ended), so
+    // the exact distances hold only the candidates' rows in registers (occupancy) and do not
+    // re-load x_i per sweep.  Lanes past d re-read the row's first 16 B (in bounds; the features
+    // past d are masked at use).
     if constexpr (XL) {
         const float* xg = X + size_t(i) * d;
 #pragma unroll
         for (int q = 0; q < XQ; ++q) {
             const int k = 4 * lane + 256 * q;
-            xr[q] = k < d ? *reinterpret_cast<const f32x4*>(xg + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+            __builtin_amdgcn_global_load_lds(xg + (k < d ? k : 0), (lds_void*)&s_xi[wv][256 * q],
+                                             16, 0, 0);
         }
     }
 
@@ -1512,11 +1513,6 @@ void knn_select_kernel(
         constexpr int TOP = KC == 16 ? 2 : (KC == 32 ? 3 : 4);
         const bool redo = select_threshold<TOP, NP, CH, H>(row, plane, n, ld, i, kc, s_cand[wv],
                                                            s_cgd[wv], ci, kce, tb, gb, vrow);
-        if constexpr (XL) {
-#pragma unroll
-            for (int q = 0; q < XQ; ++q)
-                *reinterpret_cast<f32x4*>(&s_xi[wv][4 * lane + 256 * q]) = xr[q];
-        }
         GLL_TRACE_PT(17);
         if (redo) {
             if (lane == 0) atomicAdd(&status_pub[GLL_ST_KNN_MERGE], 1);
@@ -1564,7 +1560,10 @@ void knn_select_kernel(
     // 3) exact squared distances of the candidates, fp32.  PG passes per sweep for single
     //    graphs (one wave per SIMD anyway); batches keep PG = 1 (register pressure).
     const float* xi = X + size_t(i) * d;
-    __builtin_amdgcn_wave_barrier();   // the LDS copy of x_i (written above) is complete
+    // the LDS-DMA copy of x_i (issued at entry) has landed: DMA writes count in vmcnt, which
+    // the compiler does not track for them
+    if constexpr (XL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
     double ce = double(exact_d2<VEC, PG, float, NU, XL>(X, xi, i, d, ci, 0, kce,
                                                         __builtin_inff(), &s_xi[wv][0]));
@@ -2213,6 +2212,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     // 255 us).  GLL_KNOB_SEL_FORM 1 / 2 forces either (tests, A/B).
     const int form = knob(GLL_KNOB_SEL_FORM);
     const bool lat = bt.B == 1 && (form == 1 || (form == 0 && rows <= 2048));
+    const bool occ8 = form == 3;
     prof_begin(GLL_K_SELECT, s);
 // Batched launches (PG = 1) stage x_i in LDS (XQ quarters of 256 features, d <= 1024) and run at
 // 6 waves per SIMD: measured at B = 64 NS, select 259 -> 214 us (XQ = 2, NU = 8; the NU = 16
@@ -2224,6 +2224,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
 // once the kernel took its graph index once instead of per pointer.
 #define GLL_SEL6(KCV, V, NPV, NUS, NUB, XQV, CHV, HV)                                          \
     launch_k((lat ? knn_select_kernel<KCV, V, NPV, 2, NUS, 0, false, CHV, HV>            \
+                  : occ8 ? knn_select_kernel<KCV, V, NPV, 1, 4, (V ? XQV : 0), true, CHV, HV> \
                         : knn_select_kernel<KCV, V, NPV, 1, NUB, (V ? XQV : 0), true, CHV, HV>), grid, 256, 0, s, \
         L.at<float>(ws, L.D2), L.ldD, plane, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0,     \
         L.RCAP,                                                                                \
