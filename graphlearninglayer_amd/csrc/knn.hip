@@ -2212,19 +2212,19 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     // 255 us).  GLL_KNOB_SEL_FORM 1 / 2 forces either (tests, A/B).
     const int form = knob(GLL_KNOB_SEL_FORM);
     const bool lat = bt.B == 1 && (form == 1 || (form == 0 && rows <= 2048));
-    const bool occ8 = form == 3;
     prof_begin(GLL_K_SELECT, s);
-// Batched launches (PG = 1) stage x_i in LDS (XQ quarters of 256 features, d <= 1024) and run at
-// 6 waves per SIMD: measured at B = 64 NS, select 259 -> 214 us (XQ = 2, NU = 8; the NU = 16
-// batch of loads held 120 VGPRs, 4 waves).  NU: 32-feature steps per exact-distance load batch,
-// d / 32 up to 8 for batches (16 for single graphs, whose one wave per SIMD has registers to
-// spare); the loads of steps past d are clamped to row 0 and masked.
+// Batched launches (PG = 1) stage x_i in LDS (XQ quarters of 256 features, d <= 1024): round 2
+// measured B = 64 NS select 259 -> 214 us at 6 waves per SIMD (XQ = 2, NU = 8; the NU = 16
+// batch of loads held 120 VGPRs, 4 waves).  Round 4 (x_i by LDS-DMA, no registers held for it):
+// NU = 4 at 8 waves per SIMD, B = 64 NS 183 -> 174 us, FullySup B = 64 349 -> 339, stress
+// 169 -> 168 (profiles/r04q_ab_sel.txt).  NU: 32-feature steps per exact-distance load batch
+// (16 for the latency form, whose two waves per SIMD have registers to spare); the loads of
+// steps past d are clamped to row 0 and masked.
 // Batched launches number blocks XCD-contiguously (R = true: each XCD works through a run of
 // graphs): NS B = 64 220 -> 213 us, FullySup B = 64 440 -> 429 us (profiles/r02h_xcd_ab.txt),
 // once the kernel took its graph index once instead of per pointer.
 #define GLL_SEL6(KCV, V, NPV, NUS, NUB, XQV, CHV, HV)                                          \
     launch_k((lat ? knn_select_kernel<KCV, V, NPV, 2, NUS, 0, false, CHV, HV>            \
-                  : occ8 ? knn_select_kernel<KCV, V, NPV, 1, 4, (V ? XQV : 0), true, CHV, HV> \
                         : knn_select_kernel<KCV, V, NPV, 1, NUB, (V ? XQV : 0), true, CHV, HV>), grid, 256, 0, s, \
         L.at<float>(ws, L.D2), L.ldD, plane, X, n, L.d, K, kc, eps_fixed, auto_eps ? 1 : 0,     \
         L.RCAP,                                                                                \
@@ -2248,9 +2248,9 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     do {                                                                                       \
         if (planes == 2) GLL_SEL4(KCV, V, 2, 16, 16, 0);                                       \
         else if (L.d <= 128) GLL_SEL4(KCV, V, 1, 4, 4, 1);                                     \
-        else if (L.d <= 256) GLL_SEL4(KCV, V, 1, 16, 8, 1);                                    \
-        else if (L.d <= 512) GLL_SEL4(KCV, V, 1, 16, 8, 2);                                    \
-        else if (L.d <= 1024) GLL_SEL4(KCV, V, 1, 16, 8, 4);                                   \
+        else if (L.d <= 256) GLL_SEL4(KCV, V, 1, 16, 4, 1);                                    \
+        else if (L.d <= 512) GLL_SEL4(KCV, V, 1, 16, 4, 2);                                    \
+        else if (L.d <= 1024) GLL_SEL4(KCV, V, 1, 16, 4, 4);                                   \
         else GLL_SEL4(KCV, V, 1, 16, 16, 0);                                                   \
     } while (0)
     if (KC == 16) { if (vec) GLL_SEL(16, true); else GLL_SEL(16, false); }
