@@ -731,17 +731,21 @@ __device__ __forceinline__ void supertile_tile(int t, int T, int& bi, int& bj) {
 
 // One-dimensional grid over B graphs x T (T + 1) / 2 tiles: xcd_tile deals each XCD a
 // contiguous run of the graph-major sequence, so a batch's graphs are XCD-local too.
-// t0 >= 0 (the tail of a 256-tile launch, launch_gram): block 4 j + s computes 128-subtile s of
-// 256-tile t0 + j in gram_pk2_kernel's sequence (T2 = ceil(T / 2) blocks a side); subtiles below
-// a diagonal 256-tile's diagonal or past n return at once.
+// t0 >= 0 (the tail of a 256-tile launch, launch_gram): block (4 j + s) KS + q computes
+// 128-subtile s of 256-tile t0 + j in gram_pk2_kernel's sequence (T2 = ceil(T / 2) blocks a
+// side) over k-stage slice q of KS; subtiles below a diagonal 256-tile's diagonal or past n
+// return at once.  KS > 1: the raw products go to part[block][128][128] for
+// gram_tail_reduce_kernel instead of the epilogue.
 template <bool H>
 __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__ Ph,
                                                       const __bf16* __restrict__ Pl,
                                                       const float* __restrict__ nrm, int n,
                                                       int dp, int T, float* __restrict__ D2,
                                                       int ld, size_t wss,
-                                                      float* __restrict__ d2s, int t0) {
-    int g, bi, bj;
+                                                      float* __restrict__ d2s, int t0, int KS,
+                                                      float* __restrict__ part) {
+    const int nks = dp / kPK;
+    int g, bi, bj, k0 = 0, k1 = nks;
     if (t0 < 0) {
         const int NT = T * (T + 1) / 2;
         const int idx = xcd_tile(blockIdx.x, gridDim.x);
@@ -749,7 +753,10 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
         supertile_tile(idx - g * NT, T, bi, bj);
     } else {
         const int T2 = (T + 1) / 2, NT2 = T2 * (T2 + 1) / 2;
-        const int idx2 = t0 + int(blockIdx.x >> 2), sub = int(blockIdx.x & 3);
+        const int tb = int(blockIdx.x) / KS, q = int(blockIdx.x) % KS;
+        const int idx2 = t0 + (tb >> 2), sub = tb & 3;
+        k0 = q * nks / KS;
+        k1 = (q + 1) * nks / KS;
         int b2i, b2j;
         g = idx2 / NT2;
         supertile_tile(idx2 - g * NT2, T2, b2i, b2j);
@@ -804,25 +811,24 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
         const int pos = (2 * kk + h) ^ ((row >> 1) & 7);
         return *reinterpret_cast<const bf16x8*>(sm + (buf * 4 + pl) * kTP + row * kPK + 8 * pos);
     };
-    const int nks = dp / kPK;
     // One wave per SIMD: the next stage's 16 DMAs are issued in four groups between this
     // stage's MFMA groups, so their issue overlaps the MFMA pipe.  One barrier per stage: it
     // orders stage ks's DMAs (each wave drained its own with vmcnt(0) first) before any
     // fragment read, and every wave's reads of the buffer the next DMAs overwrite (stage ks-1's)
     // before those DMAs are issued.
 #pragma unroll
-    for (int q0 = 0; q0 < 16; q0 += 4) issue4(0, 0, q0);
+    for (int q0 = 0; q0 < 16; q0 += 4) issue4(k0, 0, q0);
     float dsc = 1.f;   // fp16 D2 scale (H), computed under the first stage's DMAs
     if constexpr (H) {
         __shared__ float red[4];
         dsc = tile_d2_scale<256>(nrm, n, red);
         if (threadIdx.x == 0) *d2s = dsc;
     }
-    for (int ks = 0; ks < nks; ++ks) {
-        const int buf = ks & 1;
+    for (int ks = k0; ks < k1; ++ks) {
+        const int buf = (ks - k0) & 1;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's stage-ks DMAs
         __builtin_amdgcn_s_barrier();                          // every wave's
-        const bool more = ks + 1 < nks;
+        const bool more = ks + 1 < k1;
 #pragma unroll
         for (int kk = 0; kk < kPK / 16; ++kk) {
             if (more) issue4(ks + 1, buf ^ 1, 4 * kk);
@@ -843,6 +849,18 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
                 }
         }
+    }
+    if (KS > 1) {   // a k-slice of a tail subtile: raw products, tile-row-major
+        float* pp = part + size_t(blockIdx.x) * (128 * 128);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    pp[(wr * 64 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * 128 + wc * 64 + b * 32 + r] =
+                        acc[a][b][e];
+        return;
     }
     __syncthreads();   // the last stage's reads are done before the diagonal epilogue reuses sm
     // epilogue: D2 = |a_i|^2 + |a_j|^2 - 2 <a_i, a_j>; C layout of 32x32: col = lane & 31,
@@ -909,6 +927,53 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
             const int ti = q >> 7, tj = q & 127;
             const int i = bi * 128 + ti, j = bi * 128 + tj;
             if (i < n && j < n) dput<H>(D2, size_t(i) * ld + j, tj >= ti ? tile[ti * 129 + tj] : tile[tj * 129 + ti], dsc);
+        }
+    }
+}
+
+// The k-slices of the tail subtiles summed in slice order, then gram_pk_kernel's epilogue:
+// D2 = |a_i|^2 + |a_j|^2 - 2 <a_i, a_j> in both orientations (a diagonal subtile from its upper
+// triangle).  Block tb: subtile tb of the tail (part blocks tb KS .. tb KS + KS - 1).  Single
+// graphs only.
+template <bool H>
+__global__ __launch_bounds__(256) void gram_tail_reduce_kernel(const float* __restrict__ nrm,
+                                                               int n, int T,
+                                                               float* __restrict__ D2, int ld,
+                                                               const float* __restrict__ part,
+                                                               int KS, int t0,
+                                                               float* __restrict__ d2s) {
+    const int T2 = (T + 1) / 2;
+    const int tb = int(blockIdx.x);
+    int b2i, b2j;
+    supertile_tile(t0 + (tb >> 2), T2, b2i, b2j);
+    const int bi = 2 * b2i + ((tb & 3) >> 1), bj = 2 * b2j + (tb & 1);
+    if (bi > bj || bj >= T) return;
+    float dsc = 1.f;
+    if constexpr (H) {
+        __shared__ float red[4];
+        dsc = tile_d2_scale<256>(nrm, n, red);
+    }
+    const float* pp = part + size_t(tb) * KS * (128 * 128);
+    auto acc_at = [&](int ti, int tj) {
+        float v = pp[ti * 128 + tj];
+        for (int q = 1; q < KS; ++q) v += pp[size_t(q) * (128 * 128) + ti * 128 + tj];
+        return v;
+    };
+    for (int e = threadIdx.x; e < 128 * 128; e += 256) {
+        const int r0 = e >> 7, c0 = e & 127;
+        if (bi == bj) {   // row r0, column c0 from the upper triangle
+            const int ta = r0 < c0 ? r0 : c0, tc = r0 < c0 ? c0 : r0;
+            const int i = bi * 128 + r0, j = bi * 128 + c0;
+            if (i < n && j < n)
+                dput<H>(D2, size_t(i) * ld + j,
+                        nrm[bi * 128 + ta] + nrm[bi * 128 + tc] - 2.f * acc_at(ta, tc), dsc);
+        } else {
+            const int i = bi * 128 + r0, j = bj * 128 + c0;   // direct
+            if (i < n && j < n)
+                dput<H>(D2, size_t(i) * ld + j, nrm[i] + nrm[j] - 2.f * acc_at(r0, c0), dsc);
+            const int i2 = bi * 128 + c0, j2 = bj * 128 + r0;  // mirrored: row j2, column i2
+            if (i2 < n && j2 < n)
+                dput<H>(D2, size_t(j2) * ld + i2, nrm[i2] + nrm[j2] - 2.f * acc_at(c0, r0), dsc);
         }
     }
 }
@@ -2022,6 +2087,7 @@ __global__ __launch_bounds__(1024) void order_perm_kernel(int n, const int32_t* 
     const int pv = tid & (kPiv - 1), grp = tid / kPiv;
     const int b0 = grp * per, b1 = min(nb, b0 + per);
     int run = 0;
+#pragma unroll 8
     for (int b = b0; b < b1; ++b) run += hist[size_t(b) * kPiv + pv];
     part[grp][pv] = run;
     __syncthreads();
@@ -2044,6 +2110,7 @@ __global__ __launch_bounds__(1024) void order_perm_kernel(int n, const int32_t* 
     }
     __syncthreads();
     int o = goff[grp][pv];
+#pragma unroll 8
     for (int b = b0; b < b1; ++b) {
         const size_t q = size_t(b) * kPiv + pv;
         const int h = hist[q];
@@ -2051,9 +2118,24 @@ __global__ __launch_bounds__(1024) void order_perm_kernel(int n, const int32_t* 
         o += h;
     }
     __syncthreads();   // the offsets are visible to the whole workgroup
-    for (int i = tid; i < n; i += 1024) {
-        const int v = pid[i];
-        perm[hist[size_t(i >> 6) * kPiv + (v & 0xFF)] + (v >> 8)] = i;
+    constexpr int U = 8;   // rows per thread per batch: every load of a batch in flight together
+    for (int i0 = 0; i0 < n; i0 += 1024 * U) {
+        int v[U], h[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * 1024 + tid;
+            v[u] = i < n ? pid[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * 1024 + tid;
+            h[u] = i < n ? hist[size_t(i >> 6) * kPiv + (v[u] & 0xFF)] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * 1024 + tid;
+            if (i < n) perm[h[u] + (v[u] >> 8)] = i;
+        }
     }
 }
 
@@ -2118,8 +2200,18 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         const int cus = device_cus();
         int64_t tail = t256 && nt2 > cus ? nt2 % cus : 0;
         if (tail * 4 > cus || knob(GLL_KNOB_GRAM_TAIL) == 1) tail = 0;
+        // ... and a single graph's subtiles split over k-slices (a power of two, gram_tail_reduce
+        // sums them): stress 16 tail tiles -> 64 subtiles x 4 slices, one round.  The partial
+        // products live in the row build's staging and CSR regions (written only after the kNN)
+        int KS = 1;
+        const size_t part_cap = L.deg - L.tmp_col;   // tmp_col .. d2e, contiguous
+        if (tail > 0 && bt.B == 1 && knob(GLL_KNOB_GRAM_TAIL) != 2) {
+            while (KS * 2 <= L.dp / kPK && 4 * tail * KS * 2 <= cus &&
+                   size_t(4 * tail * KS * 2) * 128 * 128 * 4 <= part_cap)
+                KS *= 2;
+        }
         prof_begin(GLL_K_GRAM, s);
-        prof_span(tail > 0 ? 3 : 2);
+        prof_span(tail > 0 ? (KS > 1 ? 4 : 3) : 2);
         const dim3 sgrid((L.n + 3) / 4, bt.B);
         float* d2s = L.at<float>(ws, L.d2s);
         if (vec)
@@ -2130,14 +2222,19 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
             launch_k(H ? gram_pk2_kernel<true> : gram_pk2_kernel<false>,
                      dim3(unsigned(nt2 - tail)), 512, 0, s, Ph, Pl, nrm, L.n, L.dp, T2, D2,
                      L.ldD, bt.ws, d2s);
+            float* part = L.at<float>(ws, L.tmp_col);
             if (tail > 0)
                 launch_k(H ? gram_pk_kernel<true> : gram_pk_kernel<false>,
-                         dim3(unsigned(4 * tail)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T, D2, L.ldD,
-                         bt.ws, d2s, int(nt2 - tail));
+                         dim3(unsigned(4 * tail * KS)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T, D2,
+                         L.ldD, bt.ws, d2s, int(nt2 - tail), KS, part);
+            if (KS > 1)
+                launch_k(H ? gram_tail_reduce_kernel<true> : gram_tail_reduce_kernel<false>,
+                         dim3(unsigned(4 * tail)), 256, 0, s, static_cast<const float*>(nrm), L.n, T,
+                         D2, L.ldD, static_cast<const float*>(part), KS, int(nt2 - tail), d2s);
         } else {
             launch_k(H ? gram_pk_kernel<true> : gram_pk_kernel<false>,
                      dim3(unsigned(bt.B * T * (T + 1) / 2)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T,
-                     D2, L.ldD, bt.ws, d2s, -1);
+                     D2, L.ldD, bt.ws, d2s, -1, 1, static_cast<float*>(nullptr));
         }
         prof_end(GLL_K_GRAM, s);
         return launch_status("knn.hip:launch_gram(pk)");
