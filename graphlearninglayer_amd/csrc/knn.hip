@@ -731,21 +731,18 @@ __device__ __forceinline__ void supertile_tile(int t, int T, int& bi, int& bj) {
 
 // One-dimensional grid over B graphs x T (T + 1) / 2 tiles: xcd_tile deals each XCD a
 // contiguous run of the graph-major sequence, so a batch's graphs are XCD-local too.
-// t0 >= 0 (the tail of a 256-tile launch, launch_gram): block (4 j + s) KS + q computes
-// 128-subtile s of 256-tile t0 + j in gram_pk2_kernel's sequence (T2 = ceil(T / 2) blocks a
-// side) over k-stage slice q of KS; subtiles below a diagonal 256-tile's diagonal or past n
-// return at once.  KS > 1: the raw products go to part[block][128][128] for
-// gram_tail_reduce_kernel instead of the epilogue.
+// t0 >= 0 (the tail of a 256-tile launch, launch_gram): block 4 j + s computes 128-subtile s of
+// 256-tile t0 + j in gram_pk2_kernel's sequence (T2 = ceil(T / 2) blocks a side); subtiles below
+// a diagonal 256-tile's diagonal or past n return at once.
 template <bool H>
 __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__ Ph,
                                                       const __bf16* __restrict__ Pl,
                                                       const float* __restrict__ nrm, int n,
                                                       int dp, int T, float* __restrict__ D2,
                                                       int ld, size_t wss,
-                                                      float* __restrict__ d2s, int t0, int KS,
-                                                      float* __restrict__ part) {
+                                                      float* __restrict__ d2s, int t0) {
     const int nks = dp / kPK;
-    int g, bi, bj, k0 = 0, k1 = nks;
+    int g, bi, bj;
     if (t0 < 0) {
         const int NT = T * (T + 1) / 2;
         const int idx = xcd_tile(blockIdx.x, gridDim.x);
@@ -753,10 +750,7 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
         supertile_tile(idx - g * NT, T, bi, bj);
     } else {
         const int T2 = (T + 1) / 2, NT2 = T2 * (T2 + 1) / 2;
-        const int tb = int(blockIdx.x) / KS, q = int(blockIdx.x) % KS;
-        const int idx2 = t0 + (tb >> 2), sub = tb & 3;
-        k0 = q * nks / KS;
-        k1 = (q + 1) * nks / KS;
+        const int idx2 = t0 + int(blockIdx.x >> 2), sub = int(blockIdx.x & 3);
         int b2i, b2j;
         g = idx2 / NT2;
         supertile_tile(idx2 - g * NT2, T2, b2i, b2j);
@@ -817,18 +811,18 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
     // fragment read, and every wave's reads of the buffer the next DMAs overwrite (stage ks-1's)
     // before those DMAs are issued.
 #pragma unroll
-    for (int q0 = 0; q0 < 16; q0 += 4) issue4(k0, 0, q0);
+    for (int q0 = 0; q0 < 16; q0 += 4) issue4(0, 0, q0);
     float dsc = 1.f;   // fp16 D2 scale (H), computed under the first stage's DMAs
     if constexpr (H) {
         __shared__ float red[4];
         dsc = tile_d2_scale<256>(nrm, n, red);
         if (threadIdx.x == 0) *d2s = dsc;
     }
-    for (int ks = k0; ks < k1; ++ks) {
-        const int buf = (ks - k0) & 1;
+    for (int ks = 0; ks < nks; ++ks) {
+        const int buf = ks & 1;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's stage-ks DMAs
         __builtin_amdgcn_s_barrier();                          // every wave's
-        const bool more = ks + 1 < k1;
+        const bool more = ks + 1 < nks;
 #pragma unroll
         for (int kk = 0; kk < kPK / 16; ++kk) {
             if (more) issue4(ks + 1, buf ^ 1, 4 * kk);
@@ -849,18 +843,6 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
                 }
         }
-    }
-    if (KS > 1) {   // a k-slice of a tail subtile: raw products, tile-row-major
-        float* pp = part + size_t(blockIdx.x) * (128 * 128);
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int e = 0; e < 16; ++e)
-                    pp[(wr * 64 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * 128 + wc * 64 + b * 32 + r] =
-                        acc[a][b][e];
-        return;
     }
     __syncthreads();   // the last stage's reads are done before the diagonal epilogue reuses sm
     // epilogue: D2 = |a_i|^2 + |a_j|^2 - 2 <a_i, a_j>; C layout of 32x32: col = lane & 31,
@@ -931,53 +913,6 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
     }
 }
 
-// The k-slices of the tail subtiles summed in slice order, then gram_pk_kernel's epilogue:
-// D2 = |a_i|^2 + |a_j|^2 - 2 <a_i, a_j> in both orientations (a diagonal subtile from its upper
-// triangle).  Block tb: subtile tb of the tail (part blocks tb KS .. tb KS + KS - 1).  Single
-// graphs only.
-template <bool H>
-__global__ __launch_bounds__(256) void gram_tail_reduce_kernel(const float* __restrict__ nrm,
-                                                               int n, int T,
-                                                               float* __restrict__ D2, int ld,
-                                                               const float* __restrict__ part,
-                                                               int KS, int t0,
-                                                               float* __restrict__ d2s) {
-    const int T2 = (T + 1) / 2;
-    const int tb = int(blockIdx.x);
-    int b2i, b2j;
-    supertile_tile(t0 + (tb >> 2), T2, b2i, b2j);
-    const int bi = 2 * b2i + ((tb & 3) >> 1), bj = 2 * b2j + (tb & 1);
-    if (bi > bj || bj >= T) return;
-    float dsc = 1.f;
-    if constexpr (H) {
-        __shared__ float red[4];
-        dsc = tile_d2_scale<256>(nrm, n, red);
-    }
-    const float* pp = part + size_t(tb) * KS * (128 * 128);
-    auto acc_at = [&](int ti, int tj) {
-        float v = pp[ti * 128 + tj];
-        for (int q = 1; q < KS; ++q) v += pp[size_t(q) * (128 * 128) + ti * 128 + tj];
-        return v;
-    };
-    for (int e = threadIdx.x; e < 128 * 128; e += 256) {
-        const int r0 = e >> 7, c0 = e & 127;
-        if (bi == bj) {   // row r0, column c0 from the upper triangle
-            const int ta = r0 < c0 ? r0 : c0, tc = r0 < c0 ? c0 : r0;
-            const int i = bi * 128 + r0, j = bi * 128 + c0;
-            if (i < n && j < n)
-                dput<H>(D2, size_t(i) * ld + j,
-                        nrm[bi * 128 + ta] + nrm[bi * 128 + tc] - 2.f * acc_at(ta, tc), dsc);
-        } else {
-            const int i = bi * 128 + r0, j = bj * 128 + c0;   // direct
-            if (i < n && j < n)
-                dput<H>(D2, size_t(i) * ld + j, nrm[i] + nrm[j] - 2.f * acc_at(r0, c0), dsc);
-            const int i2 = bi * 128 + c0, j2 = bj * 128 + r0;  // mirrored: row j2, column i2
-            if (i2 < n && j2 < n)
-                dput<H>(D2, size_t(j2) * ld + i2, nrm[i2] + nrm[j2] - 2.f * acc_at(c0, r0), dsc);
-        }
-    }
-}
-
 // --------------------------------------------------------------------------------------
 // K1b: per-row selection + exact re-rank + reverse scatter
 // --------------------------------------------------------------------------------------
@@ -991,8 +926,9 @@ struct D2Row {
         if constexpr (H) {
             const h16x4 v = *reinterpret_cast<const h16x4*>(base + 2 * e);
             return f32x4{float(v.x) * inv, float(v.y) * inv, float(v.z) * inv, float(v.w) * inv};
-        } else {
-            return *reinterpret_cast<const f32x4*>(base + 4 * e);
+        } else {   // streamed once per select: nontemporal (stress select 171 -> 153 us,
+                   // profiles/r04s_ab_nt.txt)
+            return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(base + 4 * e));
         }
     }
     __device__ __forceinline__ float ld1(size_t e) const {
@@ -2200,18 +2136,10 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         const int cus = device_cus();
         int64_t tail = t256 && nt2 > cus ? nt2 % cus : 0;
         if (tail * 4 > cus || knob(GLL_KNOB_GRAM_TAIL) == 1) tail = 0;
-        // ... and a single graph's subtiles split over k-slices (a power of two, gram_tail_reduce
-        // sums them): stress 16 tail tiles -> 64 subtiles x 4 slices, one round.  The partial
-        // products live in the row build's staging and CSR regions (written only after the kNN)
-        int KS = 1;
-        const size_t part_cap = L.deg - L.tmp_col;   // tmp_col .. d2e, contiguous
-        if (tail > 0 && bt.B == 1 && knob(GLL_KNOB_GRAM_TAIL) != 2) {
-            while (KS * 2 <= L.dp / kPK && 4 * tail * KS * 2 <= cus &&
-                   size_t(4 * tail * KS * 2) * 128 * 128 * 4 <= part_cap)
-                KS *= 2;
-        }
+        // (Measured and dropped: the subtiles split further over 4 k-slices summed by a reduce
+        // kernel, 256 workgroups instead of 64: 250 -> 260 us, profiles/r04u_ab_tail.txt.)
         prof_begin(GLL_K_GRAM, s);
-        prof_span(tail > 0 ? (KS > 1 ? 4 : 3) : 2);
+        prof_span(tail > 0 ? 3 : 2);
         const dim3 sgrid((L.n + 3) / 4, bt.B);
         float* d2s = L.at<float>(ws, L.d2s);
         if (vec)
@@ -2222,19 +2150,14 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
             launch_k(H ? gram_pk2_kernel<true> : gram_pk2_kernel<false>,
                      dim3(unsigned(nt2 - tail)), 512, 0, s, Ph, Pl, nrm, L.n, L.dp, T2, D2,
                      L.ldD, bt.ws, d2s);
-            float* part = L.at<float>(ws, L.tmp_col);
             if (tail > 0)
                 launch_k(H ? gram_pk_kernel<true> : gram_pk_kernel<false>,
-                         dim3(unsigned(4 * tail * KS)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T, D2,
-                         L.ldD, bt.ws, d2s, int(nt2 - tail), KS, part);
-            if (KS > 1)
-                launch_k(H ? gram_tail_reduce_kernel<true> : gram_tail_reduce_kernel<false>,
-                         dim3(unsigned(4 * tail)), 256, 0, s, static_cast<const float*>(nrm), L.n, T,
-                         D2, L.ldD, static_cast<const float*>(part), KS, int(nt2 - tail), d2s);
+                         dim3(unsigned(4 * tail)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T, D2, L.ldD,
+                         bt.ws, d2s, int(nt2 - tail));
         } else {
             launch_k(H ? gram_pk_kernel<true> : gram_pk_kernel<false>,
                      dim3(unsigned(bt.B * T * (T + 1) / 2)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T,
-                     D2, L.ldD, bt.ws, d2s, -1, 1, static_cast<float*>(nullptr));
+                     D2, L.ldD, bt.ws, d2s, -1);
         }
         prof_end(GLL_K_GRAM, s);
         return launch_status("knn.hip:launch_gram(pk)");

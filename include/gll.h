@@ -93,7 +93,7 @@ extern "C" {
 #define GLL_KNOB_GRID_CAP 1   /* whole-GPU CG: co-resident workgroup capacity */
 #define GLL_KNOB_GRAM_TILE 2  /* pre-split Gram: 128- or 256-row tiles */
 #define GLL_KNOB_SEL_FORM 3   /* kNN select form: 1 latency (PG 2), 2 occupancy (knn.hip) */
-#define GLL_KNOB_GRAM_TAIL 4  /* Gram tail (knn.hip): 1 none, 2 128-subtiles without k-slices */
+#define GLL_KNOB_GRAM_TAIL 4  /* 1: no 128-subtile tail after the 256-tile Gram (knn.hip) */
 #define GLL_KNOB_COUNT 5
 int gll_set_knob(int knob, int value);
 

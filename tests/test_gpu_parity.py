@@ -1089,28 +1089,26 @@ def test_gram_256_tiles_match_128_tiles(cfg, B, n_extra, d, monkeypatch):
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
 
 
-def test_gram_tail_forms_change_no_result():
-    """The stress Gram (8,192 x 1024: 528 256-tiles on 256 CUs) runs its 16-tile last round as
-    64 128-subtiles x 4 k-slices summed by gram_tail_reduce_kernel; GLL_KNOB_GRAM_TAIL = 2 runs the
-    subtiles whole, 1 runs the third 256-tile round.  D2 only nominates candidates: the kNN
-    lists, distances and eps are bitwise the same, and no row needs the exact rescan (the summed
-    slices stay inside the Gram's error bound; GLL.py:183,205)."""
+def test_gram_tail_changes_no_result():
+    """The stress Gram (8,192 x 1024: 528 256-tiles on 256 CUs) runs its 16-tile last round as 64
+    128-subtiles (gram_pk_kernel, bitwise the 256-tile kernel's D2); GLL_KNOB_GRAM_TAIL = 1 runs a
+    third 256-tile round instead.  The kNN lists, distances and eps are bitwise the same, and no
+    row needs the exact rescan (GLL.py:183,205)."""
     from graphlearninglayer_amd import _lib
     from graphlearninglayer_amd.synth import CONFIGS, synth
     c = CONFIGS["stress"]
     X, _ = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=5)
     outs = []
     try:
-        for tail in (0, 2, 1):
+        for tail in (0, 1):
             _lib.set_knob(_lib.KNOB_GRAM_TAIL, tail)
             g = _gpu_knn(X, c["k"], "auto")
             outs.append({key: g[key].cpu().numpy() for key in ("knn_idx", "knn_d2", "eps")})
             assert int(g["status"][_lib.ST_KNN_RESCAN].item()) == 0, tail
     finally:
         _lib.set_knob(_lib.KNOB_GRAM_TAIL, 0)
-    for o in outs[1:]:
-        for key in o:
-            np.testing.assert_array_equal(o[key], outs[0][key])
+    for key in outs[0]:
+        np.testing.assert_array_equal(outs[1][key], outs[0][key])
 
 
 @pytest.mark.parametrize("eps", [1.0, "auto"])
