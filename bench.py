@@ -249,8 +249,15 @@ def batched_measure(c, eps, tau, k, B, gstats, dev, rank, steps=20, warmup=5):
         step()
     torch.cuda.synchronize()
     kid = [_lib.kernel_name(q) for q in range(_lib.K_COUNT)].index("cg_kernel")
-    # every launch of every kernel bracketed (a lone bracket on the CG reads long: see main())
+    # every launch of every kernel bracketed (a lone bracket on the CG reads long: see main()); an
+    # untimed pass first fills the event pool, so the timed one creates no event
     for q in range(_lib.K_COUNT):
+        _lib.prof_enable(q, 1)
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    for q in range(_lib.K_COUNT):
+        _lib.prof_read(q)
         _lib.prof_enable(q, 1)
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -492,7 +499,12 @@ def main():
     if not a.no_profile:
         for q in range(_lib.K_COUNT):
             _lib.prof_enable(q, 1)
-        for _ in range(10):
+        # as many bracketed steps as the timed region will sample, so that every event pair it
+        # uses comes from the pool these leave behind: a hipEventCreate inside the timed region
+        # cost ~12 us each (every 7th step brackets 5 kernels: 17 us per step on average,
+        # profiles/r04v_bench_ns.json against r04a)
+        n_inst = max(10, a.steps // PROF_PERIOD + 2)
+        for _ in range(n_inst):
             step()
         gatherer.wait()
         torch.cuda.synchronize()
@@ -501,7 +513,7 @@ def main():
             _lib.prof_enable(q, 0)
             if cnt:
                 per_kernel[names[q]] = {"us_per_launch": round(1e3 * ms / cnt, 3),
-                                        "launches_per_step": cnt / 10}
+                                        "launches_per_step": cnt / n_inst}
         dominant = max(per_kernel, key=lambda kn: per_kernel[kn]["us_per_launch"]
                        * per_kernel[kn]["launches_per_step"])
         # inside the timed region: bracket every PROF_PERIOD-th launch of every kernel (each
