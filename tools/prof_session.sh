@@ -1,6 +1,6 @@
 # Round-4 profile session (GPU box): rocprofv3 kernel stats of the shipped paths, PMC byte
 # passes (FETCH_SIZE / WRITE_SIZE, separate runs) and the Gram's MFMA counters.
-#   bash tools/r04_prof.sh <tag>     -> gpurun_out/<tag>_*  (copy the summaries to profiles/)
+#   bash tools/prof_session.sh <tag>     -> gpurun_out/<tag>_*  (copy the summaries to profiles/)
 T=${1:-r04}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && R=$PWD
 P="rocprofv3"
