@@ -386,9 +386,9 @@ def test_batched_auto_eps_matches_oracle(cfg, B):
 
 
 def test_batched_duplicates_match_single_calls():
-    """Batched selection (x_i staged in LDS, 6 waves per SIMD) on graphs with > 64 tied
-    candidates, where the exact merge runs: each graph's kNN, U and grad_X agree with its
-    single call (whose selection keeps x_i in registers)."""
+    """Batched selection (the occupancy form: x_i staged in LDS, 8 waves per SIMD) on graphs with
+    > 64 tied candidates, where the full-row fallback runs: each graph's kNN, U and grad_X agree
+    with its single call (the latency form)."""
     GLL = _gll()
     rng = np.random.default_rng(8)
     n, d, base, k, B = 600, 40, 100, 10, 2
