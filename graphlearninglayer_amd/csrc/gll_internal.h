@@ -171,7 +171,7 @@ size_t grid_cg_workspace_floats(int m, int C);
 // The whole-GPU CG's sync words at the start of its region (gridcg.hip kSyncWords): row_build
 // zeroes them before a forward whose solves take that kernel (grid_cg_route), and each solve
 // leaves them zero, so its launch needs no memset.
-constexpr int kGridSyncWords = 640;
+constexpr int kGridSyncWords = 2048;   // >= gridcg.hip kSyncWords
 struct Layout;
 int ell_emit(const Layout& L, int B);
 

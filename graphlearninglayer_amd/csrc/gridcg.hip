@@ -551,9 +551,14 @@ constexpr int kGvMaxRows = 512;       // rows per workgroup: NG x RPG <= 64 x 8
 constexpr int kSyncLine = 32;         // words per sync word (one 128-B line each)
 // sync lines: [0, 8) group arrival counters, 8 top counter, 9 failure, 10 rescue, [11, 19)
 // release words (one per group), 19 exit counter
-constexpr int kSyncTop = 8, kSyncFail = 9, kSyncRescue = 10, kSyncRel = 11, kSyncExit = 19;
-constexpr int kSyncWords = 20 * kSyncLine;
-static_assert(kSyncWords == kGridSyncWords, "gll_internal.h kGridSyncWords (row_build zeroes them)");
+#ifndef GLL_GV_GROUPS
+#define GLL_GV_GROUPS 8
+#endif
+constexpr int kGvGroups = GLL_GV_GROUPS;   // arrival groups of the two-level barrier
+constexpr int kSyncTop = kGvGroups, kSyncFail = kGvGroups + 1, kSyncRescue = kGvGroups + 2,
+              kSyncRel = kGvGroups + 3, kSyncExit = 2 * kGvGroups + 3;
+constexpr int kSyncWords = (2 * kGvGroups + 4) * kSyncLine;
+static_assert(kSyncWords <= kGridSyncWords, "gll_internal.h kGridSyncWords (row_build zeroes them)");
 
 struct GvArgs {
     int m, C, Cp, NQ, PW, max_iter;   // PW: partial floats per workgroup (32 or 64)
@@ -597,7 +602,7 @@ __device__ __forceinline__ bool gv_barrier(unsigned* sync, unsigned epoch, int G
         unsigned* top = sync + kSyncTop * kSyncLine;
         unsigned* fail = sync + kSyncFail * kSyncLine;
         unsigned* rel = sync + kSyncRel * kSyncLine;
-        const int ng = G < 8 ? G : 8;
+        const int ng = G < kGvGroups ? G : kGvGroups;
         const int g = int(blockIdx.x) % ng;
         bool last;
         if (hier) {
