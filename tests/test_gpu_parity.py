@@ -658,6 +658,47 @@ def test_grid_cg_oversubscribed_launch_is_refused():
     assert np.isfinite(U).all() and nc == 0
 
 
+def test_grid_cg_sync_words_reset_between_solves():
+    """The whole-GPU CG's sync words are zeroed by row_build before a forward and returned to
+    zero by the last workgroup out of every solve (gridcg.hip gv_exit) -- no memset launch.  Three
+    backward calls on one workspace after a forward give bitwise equal gradients with no failed
+    or rescued barrier; after a forward whose barrier failed (injected: the rescue solve ran), a
+    normal backward on the same workspace runs its grid solve cleanly (GLL.py:53,93)."""
+    import ctypes as ct
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import seeded_gbar
+    X, Y, k = _grid_case()
+    n, d = X.shape
+    base, C = Y.shape
+    g = seeded_gbar(n - base, C, 3)
+    U, grads, st = _fwd_bwds_c_abi(X, Y, k, 0.07, 1.0, g, backward_calls=3)
+    for gx in grads[1:]:
+        np.testing.assert_array_equal(gx, grads[0])
+    assert st[_lib.ST_SOLVE_FAILED] == 0 and st[_lib.ST_GRID_RESCUED] == 0
+    GLL = _gll()
+    lib = _lib.lib()
+    pf = GLL.make_problem(n, d, base, C, k, 0.07, 1.0, flags=_lib.FLAG_DIAG_GRID_FAIL)
+    pn = GLL.make_problem(n, d, base, C, k, 0.07, 1.0)
+    assert lib.gll_workspace_bytes(ct.byref(pf)) == lib.gll_workspace_bytes(ct.byref(pn))
+    ws = torch.empty(lib.gll_workspace_bytes(ct.byref(pn)), dtype=torch.uint8, device="cuda")
+    Ud = torch.empty(n - base, C, dtype=torch.float64, device="cuda")
+    gx = torch.empty(n, d, dtype=torch.float32, device="cuda")
+    Xd = torch.from_numpy(np.ascontiguousarray(X)).cuda()
+    Yd = torch.from_numpy(np.ascontiguousarray(Y)).cuda()
+    Gd = torch.from_numpy(np.ascontiguousarray(g)).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.check(lib.gll_forward(ct.byref(pf), Xd.data_ptr(), Yd.data_ptr(), _lib.GLL_DT_F32,
+                               ws.data_ptr(), Ud.data_ptr(), s), "gll_forward")
+    rescued = int(ws[: 4 * _lib.ST_NWORDS].view(torch.int32)[_lib.ST_GRID_RESCUED].item())
+    assert rescued >= 1
+    _lib.check(lib.gll_backward(ct.byref(pn), Xd.data_ptr(), None, 0, ws.data_ptr(),
+                                Gd.data_ptr(), _lib.GLL_DT_F64, gx.data_ptr(), s), "gll_backward")
+    st2 = ws[: 4 * _lib.ST_NWORDS].view(torch.int32).cpu().tolist()
+    assert st2[_lib.ST_GRID_RESCUED] == rescued and st2[_lib.ST_SOLVE_FAILED] == 0
+    assert O.rel_err(Ud.cpu().numpy(), U) <= 1e-5
+    assert O.rel_err(gx.cpu().numpy(), grads[0]) <= 1e-5
+
+
 def test_grid_cg_barrier_failure_is_rescued():
     """An (injected) grid-barrier failure of the whole-GPU CG (gridcg.hip): the first workgroup
     to see it solves the system alone (rescue_solve) and the others write nothing -- U still
