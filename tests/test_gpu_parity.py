@@ -174,6 +174,25 @@ def test_split_phase_gram_shapes(n, d, eps):
     assert O.rel_err(grad, O.backward(st, g)) < TOL
 
 
+@pytest.mark.parametrize("k,eps", [(13, 1.0), (14, "auto"), (29, 1.0), (30, "auto"),
+                                   (57, 1.0), (57, "auto")])
+def test_candidate_capacity_boundaries(k, eps):
+    """k at each edge of the select's candidate capacity (knn.hip launch_select: the smallest of
+    16 / 32 / 64 keeping a re-rank margin >= 4, so 13 | 14 and 29 | 30 switch lists; k = 57 is
+    the largest k include/gll.h accepts): exact kNN sets
+    and U / grad_X against the oracle, fixed and automatic eps (GLL.py:183, utils.py:574)."""
+    from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
+    X, lab = synth(120, 380, 64, r=1.0, seed=k)
+    Y = one_hot(lab[:120])
+    g = seeded_gbar(380, 10, k)
+    U, grad = _run(X, Y, 0.07, eps, k, g)
+    ind = _gpu_knn(X, k, eps)["knn_idx"].cpu().numpy()
+    assert O.knn_set_mismatch(X, ind, k) == []
+    Uo, st = O.forward(X, Y, 0.07, eps, k, knn=(ind, None))
+    assert O.rel_err(U, Uo) < TOL
+    assert O.rel_err(grad, O.backward(st, g)) < TOL
+
+
 def test_hub_row_longer_than_lds_chunk():
     """One point is a neighbour of everybody: its CSR row exceeds the 256-entry chunk."""
     rng = np.random.default_rng(0)
