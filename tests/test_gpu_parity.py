@@ -1189,7 +1189,7 @@ def test_locality_order_changes_no_result(eps):
     np.testing.assert_array_equal(g0, g1)
 
 
-@pytest.mark.parametrize("k,d", [(10, 256), (30, 1024)])
+@pytest.mark.parametrize("k,d", [(10, 256), (30, 1024), (14, 37), (57, 64)])
 def test_select_forms_agree_bitwise(k, d):
     """The kNN select's latency form (two candidate groups in flight; single graphs of at most
     2,048 rows) and its occupancy form (x_i staged in LDS, one group; larger graphs and batches),
