@@ -193,6 +193,26 @@ def test_candidate_capacity_boundaries(k, eps):
     assert O.rel_err(grad, O.backward(st, g)) < TOL
 
 
+@pytest.mark.parametrize("n,base,k", [(12, 3, 10), (8, 2, 10), (5, 1, 2), (70, 64, 10),
+                                      (66, 1, 10)])
+@pytest.mark.parametrize("eps", [1.0, "auto"])
+def test_tiny_graphs(n, base, k, eps):
+    """Graphs of a handful of points: k clipped to n (every point a neighbour: 8 points, k =
+    10), k = 2 (one neighbour, disconnected pieces held by tau), six unlabeled rows among 64
+    labeled, one labeled row among 66 -- U and grad_X against the oracle (GLL.py:183,205)."""
+    from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
+    X, lab = synth(base, n - base, 16, r=1.0, seed=n)
+    Y = one_hot(lab[:base])
+    g = seeded_gbar(n - base, 10, 3)
+    kk = min(k, n)
+    U, grad = _run(X, Y, 0.07, eps, k, g)
+    ind = _gpu_knn(X, kk, eps)["knn_idx"].cpu().numpy()
+    assert O.knn_set_mismatch(X, ind, kk) == []
+    Uo, st = O.forward(X, Y, 0.07, eps, kk, knn=(ind, None))
+    assert O.rel_err(U, Uo) < TOL
+    assert O.rel_err(grad, O.backward(st, g)) < TOL
+
+
 def test_hub_row_longer_than_lds_chunk():
     """One point is a neighbour of everybody: its CSR row exceeds the 256-entry chunk."""
     rng = np.random.default_rng(0)
