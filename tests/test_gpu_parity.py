@@ -213,6 +213,32 @@ def test_tiny_graphs(n, base, k, eps):
     assert O.rel_err(grad, O.backward(st, g)) < TOL
 
 
+@pytest.mark.parametrize("n,base,k", [(8, 2, 10), (12, 3, 10), (66, 1, 57)])
+def test_batched_tiny_graphs(n, base, k):
+    """The batched entry on three graphs of a handful of points (k clipped to n; k = 57 on 66
+    points): every graph's U and grad_X against the oracle on the GPU's own kNN lists, auto
+    eps (GLL.py:14-177)."""
+    from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
+    GLL = _gll()
+    B, kk = 3, min(k, n)
+    Xs, Ys = [], []
+    for g in range(B):
+        X, lab = synth(base, n - base, 16, r=1.0, seed=40 + g)
+        Xs.append(X)
+        Ys.append(one_hot(lab[:base]))
+    Xs, Ys = np.stack(Xs), np.stack(Ys)
+    G = np.stack([seeded_gbar(n - base, 10, 500 + g) for g in range(B)])
+    Xb = torch.from_numpy(Xs).cuda().requires_grad_(True)
+    Ub = GLL.LaplaceLearningSparseHard.apply(Xb, torch.from_numpy(Ys).cuda(), 0.07, "auto", k)
+    Ub.backward(torch.from_numpy(G).cuda())
+    for g in range(B):
+        ind = _gpu_knn(Xs[g], kk, "auto")["knn_idx"].cpu().numpy().astype(np.int64)
+        assert O.knn_set_mismatch(Xs[g], ind, kk) == []
+        Uo, st = O.forward(Xs[g], Ys[g], tau=0.07, epsilon="auto", K=kk, knn=(ind, None))
+        assert O.rel_err(Ub[g].detach().cpu().numpy(), Uo) <= TOL
+        assert O.rel_err(Xb.grad[g].cpu().numpy(), O.backward(st, G[g])) <= TOL
+
+
 def test_hub_row_longer_than_lds_chunk():
     """One point is a neighbour of everybody: its CSR row exceeds the 256-entry chunk."""
     rng = np.random.default_rng(0)
