@@ -1091,9 +1091,17 @@ __device__ __forceinline__ bool select_threshold(const D2Row<H>& row, size_t pla
 #pragma unroll
         for (int s = 0; s < TOP; ++s) top = m[s] != 0xFFFFFFFFu ? m[s] : top;
         uint32_t lo = wave_min_u32(m[0]), up = wave_max_u32(top);
-        while (lo < up) {   // smallest T with count_le(T) >= kc (wave-uniform, <= 32 steps)
+        // a T with count_le(T) >= kc (wave-uniform, <= 32 steps); one holding exactly kc list
+        // entries ends the search early -- any such T leaves the same list entries in the set
+        // (left-out columns stay covered by tb = T + 1, and the kNN is exact either way)
+        while (lo < up) {
             const uint32_t mid = lo + ((up - lo) >> 1);
-            if (count_le(mid) >= kc) up = mid;
+            const int c = count_le(mid);
+            if (c == kc) {
+                up = mid;
+                break;
+            }
+            if (c > kc) up = mid;
             else lo = mid + 1u;
         }
         T = up;
