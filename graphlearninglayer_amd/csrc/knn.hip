@@ -974,7 +974,9 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // columns are <= T, so the kc-th smallest D2 is too -- and every column with D2 bits <= T is
 // compacted into the wave's LDS slots.  Simulated at kc = 13 / n = 1,000 (TOP = 2) the set
 // averages 13.2 columns, at kc = 32 / n = 1,500 (TOP = 3) 32.4; kc = 37 / n = 8,192 (stress,
-// TOP = 4) holds ~0.6 of the kc nearest per lane.  CH > 0: the row (n <= 1024 CH) stays in
+// TOP = 5) holds ~0.6 of the kc nearest per lane -- five slots, not four, leave fewer rows
+// with a full lane list and so a second read (stress select 151 -> 145 us,
+// profiles/r04f8_ab_top5.txt).  CH > 0: the row (n <= 1024 CH) stays in
 // registers between the two passes; CH = 0 re-reads it (L2 / MALL-hot).  Returns true when more
 // than 64 columns tie in (the caller runs select_fallback, tb = T on return).  tb: D2 bits every
 // left-out column is >= to (+inf when every valid column is a candidate).
@@ -1519,7 +1521,7 @@ void knn_select_kernel(
     {
         f32x4 vrow[CH > 0 ? CH * kSelNB : 1];
         if constexpr (CH > 0) load_d2_row<NP, CH, H>(row, plane, ld, vrow);
-        constexpr int TOP = KC == 16 ? 2 : (KC == 32 ? 3 : 4);
+        constexpr int TOP = KC == 16 ? 2 : (KC == 32 ? 3 : 5);
         const bool redo = select_threshold<TOP, NP, CH, H>(row, plane, n, ld, i, kc, s_cand[wv],
                                                            s_cgd[wv], ci, kce, tb, gb, vrow);
         GLL_TRACE_PT(17);
