@@ -141,9 +141,11 @@ def _eps_value(epsilon) -> float:
         return 0.0
     e = float(epsilon)
     if not e > 0.0:
-        # the reference divides by eps (GLL.py:233): a non-positive eps yields inf/NaN
+        # GLL.py:240-241 warns for any eps < 1e-10.  The reference uses eps only as the product
+        # eps[rows] * eps[cols] (GLL.py:233-234), so a negative eps builds the graph of |eps|;
+        # eps = 0 (or NaN) divides by zero there, here it disconnects the graph (W = 0)
         warnings.warn("Epsilon in KNN is very close to zero.", UserWarning)
-        return 1e-30
+        return -e if e < 0.0 else 1e-30
     return e
 
 

@@ -27,6 +27,10 @@ constexpr int kMaxKm1 = 56;      // K - 1 <= 56: the kNN rescan keeps >= 8 lanes
 // ---------------------------------------------------------------------------------------
 constexpr int kStOvfCount = 8;   // internal status words: overflow-list length
 constexpr int kStBump = 9;       //                        bump-region cursor
+constexpr int kStPermValid = 11; //                        1: this forward wrote the locality
+                                 //                        order (order_perm_kernel); the Gram
+                                 //                        zeroes it, so a backward never reads
+                                 //                        a perm its forward did not write
 constexpr int kPiv = 64;         // pivot rows of the locality order (order_pid_kernel)
 constexpr int kStWords = GLL_ST_NWORDS;   // words the Gram kernels zero per call
 
@@ -286,6 +290,13 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+// Wall-clock bound of the in-launch waits (grid barriers, the fused backward's hand-off):
+// s_memrealtime ticks at a constant 100 MHz whatever the shader clock, so 1e8 ticks = 1 s.
+constexpr unsigned long long kWaitTicks = 100000000ull;
+__device__ __forceinline__ unsigned long long wall_ticks() {
+    return __builtin_amdgcn_s_memrealtime();
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -182,9 +182,13 @@ template <int COEF, int LPR>
 __global__ __launch_bounds__(256) void grad_chunk_kernel(EdgeArgs a, const float* __restrict__ X,
                                                          float* __restrict__ out, int nch,
                                                          size_t xs, size_t gxs,
-                                                         const int32_t* __restrict__ perm) {
+                                                         const int32_t* __restrict__ perm,
+                                                         const int32_t* __restrict__ perm_ok) {
     GLL_TRACE_SCOPE(1);
     a.to_graph();
+    // the order exists only if this workspace's forward wrote it (its flags may differ from the
+    // backward's: gll_backward takes its own gll_problem)
+    if (perm && *perm_ok != 1) perm = nullptr;
     X = gshift(X, xs);
     out = gshift(out, gxs);
     constexpr int RPW = kWave / LPR;
@@ -263,18 +267,21 @@ static bool grad_use_chunks(const Layout& L, const Batch& bt, bool vec) {
 // LPR = the power of two nearest d / 32 in [16, 64], NCH = ceil(d / (4 LPR)) chunks.
 template <int COEF>
 static void grad_chunked(const EdgeArgs& a, const Batch& bt, const float* X, float* out,
-                         const int32_t* perm, hipStream_t s) {
+                         const int32_t* perm, const int32_t* perm_ok, hipStream_t s) {
     int lpr = 16;
     while (lpr < 64 && 4 * lpr * 8 < a.d) lpr *= 2;
     const int nch = (a.d + 4 * lpr - 1) / (4 * lpr);
     const int rows_per_block = 4 * (kWave / lpr);
     dim3 grid(unsigned(nch * ((a.n + rows_per_block - 1) / rows_per_block)), bt.B);
     if (lpr == 16)
-        launch_k(grad_chunk_kernel<COEF, 16>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx, perm);
+        launch_k(grad_chunk_kernel<COEF, 16>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx, perm,
+                 perm_ok);
     else if (lpr == 32)
-        launch_k(grad_chunk_kernel<COEF, 32>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx, perm);
+        launch_k(grad_chunk_kernel<COEF, 32>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx, perm,
+                 perm_ok);
     else
-        launch_k(grad_chunk_kernel<COEF, 64>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx, perm);
+        launch_k(grad_chunk_kernel<COEF, 64>, grid, 256, 0, s, a, X, out, nch, bt.x, bt.gx, perm,
+                 perm_ok);
 }
 
 template <bool AUTO, bool VEC, int CV>
@@ -328,9 +335,13 @@ hipError_t launch_backward_grad(const Layout& L, const Batch& bt, void* ws, cons
     }
     prof_begin(GLL_K_GRAD, s);
     if (chunk) {
-        const int32_t* perm = locality_order(L, bt) ? L.at<int32_t>(ws, L.perm) : nullptr;
-        if (auto_eps) grad_chunked<1>(a, bt, X, gradX, perm, s);
-        else grad_chunked<2>(a, bt, X, gradX, perm, s);
+        // the forward's order, if it wrote one (device word: the forward's flags are not known here)
+        const bool order = bt.B == 1 && L.PR == L.n && L.n >= 16 * kPiv &&
+                           size_t(L.n) * L.d * 4 > (size_t(4) << 20);
+        const int32_t* perm = order ? L.at<int32_t>(ws, L.perm) : nullptr;
+        const int32_t* pok = L.at<int32_t>(ws, L.status) + kStPermValid;
+        if (auto_eps) grad_chunked<1>(a, bt, X, gradX, perm, pok, s);
+        else grad_chunked<2>(a, bt, X, gradX, perm, pok, s);
         e = launch_status("grad.hip:grad_chunked");
     } else if (auto_eps) {
         e = vec ? grad_nd<true, true, 0>(a, bt, X, gradX, s)

@@ -117,6 +117,7 @@ __device__ __forceinline__ bool grid_barrier(unsigned* sync, unsigned target, in
         int ok = 1;
         __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned spins = 0;
+        const unsigned long long t0 = wall_ticks();
         while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             __builtin_amdgcn_s_sleep(1);
             if ((++spins & 1023u) == 0) {
@@ -124,7 +125,7 @@ __device__ __forceinline__ bool grid_barrier(unsigned* sync, unsigned target, in
                     ok = 0;
                     break;
                 }
-                if (spins > (1u << 24)) {   // ~1 s: a workgroup never arrived
+                if (wall_ticks() - t0 > kWaitTicks) {   // 1 s: a workgroup never arrived
                     __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     ok = 0;
                     break;
@@ -293,12 +294,22 @@ __device__ void rescue_solve(const Mat& A, int m, int C, const void* b, int b_dt
     }
 }
 
-// After a grid kernel's loop: true when this workgroup wrote nothing because a barrier failed
-// (it rescued the solve, or another workgroup does).
+// After a grid kernel's loop: true when this workgroup must write nothing because a barrier
+// failed (it rescued the solve, or another workgroup does).  A workgroup whose own barriers all
+// completed can still be in that case: a late arrival completes the final barrier just after
+// another workgroup timed out on it and claimed the rescue.  Such a workgroup reads the failure
+// word and leaves the solution to the rescuer, so U is never a mix of the two solves.  (A
+// workgroup that read the word just before the timeout still writes: a rescued solve -- counted
+// in GLL_ST_GRID_RESCUED -- is correct to the CG tolerance but not bitwise reproducible.)
 template <class Mat, int NT, class Args>
-__device__ bool rescued(bool ok, unsigned* rescue_word, const Mat& A, const Args& a,
-                        float* scr, int* s_flag) {
-    if (ok) return false;
+__device__ bool rescued(bool ok, unsigned* fail_word, unsigned* rescue_word, const Mat& A,
+                        const Args& a, float* scr, int* s_flag) {
+    if (ok) {
+        if (threadIdx.x == 0)
+            *s_flag = __hip_atomic_load(fail_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        __syncthreads();
+        return *s_flag != 0;
+    }
     if (threadIdx.x == 0)
         *s_flag = __hip_atomic_fetch_add(rescue_word, 1u, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT) == 0u;
@@ -520,7 +531,7 @@ __global__ __launch_bounds__(kGT) void cg_grid_classic_kernel(Mat A, GridCgArgs 
     GLL_TRACE_PT(1);
     // a failed grid barrier (a workgroup never arrived within ~1 s): one workgroup solves the
     // system alone (rescue_solve), the others write nothing
-    if (rescued<Mat, kGT>(ok, a.sync + 2, A, a, a.rescue, &s_ok)) return;
+    if (rescued<Mat, kGT>(ok, a.sync + 1, a.sync + 2, A, a, a.rescue, &s_ok)) return;
 #pragma unroll
     for (int k = 0; k < RPG; ++k) {
         const int u = r0 + grp + k * NG;
@@ -622,6 +633,7 @@ __device__ __forceinline__ bool gv_barrier(unsigned* sync, unsigned epoch, int G
                                    __HIP_MEMORY_SCOPE_AGENT);
         int ok = 1;
         unsigned spins = 0;
+        const unsigned long long t0 = wall_ticks();
         while (__hip_atomic_load(rel + g * kSyncLine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
                epoch) {
             __builtin_amdgcn_s_sleep(1);
@@ -630,7 +642,7 @@ __device__ __forceinline__ bool gv_barrier(unsigned* sync, unsigned epoch, int G
                     ok = 0;
                     break;
                 }
-                if (spins > (1u << 24)) {   // ~1 s: a workgroup never arrived
+                if (wall_ticks() - t0 > kWaitTicks) {   // 1 s: a workgroup never arrived
                     __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     ok = 0;
                     break;
@@ -1055,7 +1067,8 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
     GLL_TRACE_PT(10);
     // a failed grid barrier (a workgroup never arrived within ~1 s): one workgroup solves the
     // system alone (rescue_solve), the others write nothing
-    if (!rescued<Mat, NT>(ok, a.sync + kSyncRescue * kSyncLine, A, a, a.rescue, &s_ok)) {
+    if (!rescued<Mat, NT>(ok, a.sync + kSyncFail * kSyncLine, a.sync + kSyncRescue * kSyncLine, A,
+                          a, a.rescue, &s_ok)) {
 #pragma unroll
         for (int k = 0; k < RPG; ++k) {
             const int uu = r0 + grp + k * NG;

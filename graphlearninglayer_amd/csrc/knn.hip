@@ -2022,7 +2022,8 @@ __global__ __launch_bounds__(256) void order_pid_kernel(const float* __restrict_
 // the histogram; then row i goes to offset[block i / 64][pivot] + its rank in the block.
 __global__ __launch_bounds__(1024) void order_perm_kernel(int n, const int32_t* __restrict__ pid,
                                                           int32_t* __restrict__ hist,
-                                                          int32_t* __restrict__ perm) {
+                                                          int32_t* __restrict__ perm,
+                                                          int32_t* __restrict__ status) {
     static_assert(kPiv == kWave, "one wave scans the pivot counts");
     constexpr int NGRP = 1024 / kPiv;   // block groups per pivot
     __shared__ int part[NGRP][kPiv];
@@ -2083,6 +2084,7 @@ __global__ __launch_bounds__(1024) void order_perm_kernel(int n, const int32_t* 
             if (i < n) perm[h[u] + (v[u] >> 8)] = i;
         }
     }
+    if (tid == 0) status[kStPermValid] = 1;   // read by the backward (grad.hip launch_backward_grad)
 }
 
 hipError_t launch_order(const Layout& L, void* ws, hipStream_t s) {
@@ -2096,7 +2098,7 @@ hipError_t launch_order(const Layout& L, void* ws, hipStream_t s) {
     else
         launch_k(order_pid_kernel<1>, grid, 256, 0, s, D2, L.ldD, plane, L.n, pid, hist);
     launch_k(order_perm_kernel, dim3(1), 1024, 0, s, L.n, static_cast<const int32_t*>(pid), hist,
-             L.at<int32_t>(ws, L.perm));
+             L.at<int32_t>(ws, L.perm), L.at<int32_t>(ws, L.status));
     return launch_status("knn.hip:launch_order");
 }
 

@@ -1087,12 +1087,13 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
         // be stale) until the next forward rebuilds it: NaN again, never a stale hand-off
         int ok = __hip_atomic_load(fsync + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
         unsigned spins = 0;
+        const unsigned long long t0 = wall_ticks();
         // ~n_poll x 256 cycles between polls: 125 workgroups polling the line the solves add
         // to would otherwise queue those adds behind a storm of loads
         while (ok && __hip_atomic_load(fsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
                unsigned(C)) {
             for (int q = 0; q < 4; ++q) __builtin_amdgcn_s_sleep(4);
-            if (++spins > (1u << 24)) {
+            if ((++spins & 15u) == 0 && wall_ticks() - t0 > kWaitTicks) {   // 1 s of wall clock
                 ok = 0;
                 break;
             }

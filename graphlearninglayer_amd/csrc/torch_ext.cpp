@@ -314,9 +314,11 @@ double parse_eps(PyObject* o) {
     }
     const double e = parse_float(o, "epsilon");
     if (!(e > 0.0)) {
-        // the reference divides by eps (GLL.py:233): a non-positive eps yields inf/NaN
+        // GLL.py:240-241 warns for any eps < 1e-10.  The reference uses eps only as the product
+        // eps[rows] * eps[cols] (GLL.py:233-234), so a negative eps builds the graph of |eps|;
+        // eps = 0 (or NaN) divides by zero there, here it disconnects the graph (W = 0)
         warn_py(PyExc_UserWarning, "Epsilon in KNN is very close to zero.");
-        return 1e-30;
+        return e < 0.0 ? -e : 1e-30;
     }
     return e;
 }

@@ -43,11 +43,11 @@ extern "C" {
                                 * and were re-ranked exactly over every column under the bound
                                 * (diagnostic count; the result is exact either way) */
 #define GLL_ST_SOLVE_FAILED 6  /* nonzero: the fused backward's gradient workgroups gave up
-                                * waiting for the adjoint solves (~1 s); the gradient was written
+                                * waiting for the adjoint solves (1 s of wall clock); the gradient was written
                                 * as NaN.  The Python layer raises RuntimeError on it */
 #define GLL_ST_KNN_MERGE 7     /* kNN rows with more than 64 columns at the threshold scan's
                                 * bound (ties): the full-row fallback ran (diagnostic count) */
-                               /* (words 8, 9 are internal) */
+                               /* (words 8, 9, 11 are internal) */
 #define GLL_ST_GRID_RESCUED 10 /* whole-GPU CG solves whose grid barrier timed out (a workgroup
                                 * was not resident: other kernels held the CUs) and that one
                                 * workgroup then solved alone -- correct, slower (count) */

@@ -868,16 +868,22 @@ def test_balanced_cg_spill_path_matches_oracle(monkeypatch):
     assert O.rel_err(gr1, O.backward(st, g)) <= TOL
 
 
-def _fwd_bwd_c_abi(X, Y, k, tau, eps, gbar, flags=0):
-    """gll_forward + gll_backward through ctypes with explicit problem flags: (U, grad_X)."""
+def _fwd_bwd_c_abi(X, Y, k, tau, eps, gbar, flags=0, bwd_flags=None, ws_fill=None):
+    """gll_forward + gll_backward through ctypes with explicit problem flags: (U, grad_X).
+    `bwd_flags`: the backward's own flags (default: the forward's); `ws_fill`: a byte value the
+    workspace holds before the forward (default: torch.empty's contents)."""
     import ctypes as ct
     from graphlearninglayer_amd import _lib
     GLL = _gll()
     n, d = X.shape
     base, C = Y.shape
     prob = GLL.make_problem(n, d, base, C, k, tau, eps, flags=flags)
+    bprob = prob if bwd_flags is None else GLL.make_problem(n, d, base, C, k, tau, eps,
+                                                            flags=bwd_flags)
     lib = _lib.lib()
     ws = torch.empty(lib.gll_workspace_bytes(ct.byref(prob)), dtype=torch.uint8, device="cuda")
+    if ws_fill is not None:
+        ws.fill_(ws_fill)
     U = torch.empty(n - base, C, dtype=torch.float64, device="cuda")
     gx = torch.empty(n, d, dtype=torch.float32, device="cuda")
     Xd = torch.from_numpy(np.ascontiguousarray(X)).cuda()
@@ -886,7 +892,7 @@ def _fwd_bwd_c_abi(X, Y, k, tau, eps, gbar, flags=0):
     s = torch.cuda.current_stream().cuda_stream
     _lib.check(lib.gll_forward(ct.byref(prob), Xd.data_ptr(), Yd.data_ptr(), _lib.GLL_DT_F32,
                                ws.data_ptr(), U.data_ptr(), s), "gll_forward")
-    _lib.check(lib.gll_backward(ct.byref(prob), Xd.data_ptr(), Yd.data_ptr(), _lib.GLL_DT_F32,
+    _lib.check(lib.gll_backward(ct.byref(bprob), Xd.data_ptr(), Yd.data_ptr(), _lib.GLL_DT_F32,
                                 ws.data_ptr(), gd.data_ptr(), _lib.GLL_DT_F64, gx.data_ptr(), s),
                "gll_backward")
     torch.cuda.synchronize()
@@ -1183,14 +1189,16 @@ def test_gram_256_tiles_match_128_tiles(cfg, B, n_extra, d, monkeypatch):
                                    for g in range(B)])).cuda()
     from graphlearninglayer_amd import _lib
     outs = []
-    for tile in (128, 256):
-        _lib.set_knob(_lib.KNOB_GRAM_TILE, tile)
-        Xb = torch.from_numpy(np.stack(Xs)).cuda().requires_grad_(True)
-        U = GLL.LaplaceLearningSparseHard.apply(Xb, torch.from_numpy(np.stack(Ys)).cuda(), 0.07,
-                                                1.0, c["k"])
-        U.backward(G)
-        outs.append((U.detach().cpu().numpy(), Xb.grad.cpu().numpy()))
-    _lib.set_knob(_lib.KNOB_GRAM_TILE, 0)
+    try:
+        for tile in (128, 256):
+            _lib.set_knob(_lib.KNOB_GRAM_TILE, tile)
+            Xb = torch.from_numpy(np.stack(Xs)).cuda().requires_grad_(True)
+            U = GLL.LaplaceLearningSparseHard.apply(Xb, torch.from_numpy(np.stack(Ys)).cuda(),
+                                                    0.07, 1.0, c["k"])
+            U.backward(G)
+            outs.append((U.detach().cpu().numpy(), Xb.grad.cpu().numpy()))
+    finally:
+        _lib.set_knob(_lib.KNOB_GRAM_TILE, 0)
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
 
@@ -1231,6 +1239,25 @@ def test_locality_order_changes_no_result(eps):
     g = seeded_gbar(c["batch"], 10, 6)
     U0, g0 = _fwd_bwd_c_abi(X, Y, c["k"], 0.07, eps, g)
     U1, g1 = _fwd_bwd_c_abi(X, Y, c["k"], 0.07, eps, g, flags=_lib.FLAG_ROW_ORDER_OFF)
+    np.testing.assert_array_equal(U0, U1)
+    np.testing.assert_array_equal(g0, g1)
+
+
+def test_backward_never_reads_an_order_its_forward_did_not_write():
+    """gll_backward takes its own gll_problem, so its flags may differ from the forward's: a
+    forward with GLL_FLAG_ROW_ORDER_OFF writes no locality order, and the backward then must not
+    gather rows through the workspace's stale perm (here all zeros: every position would map to
+    row 0, leaving the other rows of grad_X unwritten).  grad_X equals the row-order result
+    bitwise (GLL.py:146-159)."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth
+    c = CONFIGS["stress"]
+    X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=5)
+    Y = one_hot(lab[: c["base"]])
+    g = seeded_gbar(c["batch"], 10, 6)
+    off = _lib.FLAG_ROW_ORDER_OFF
+    U0, g0 = _fwd_bwd_c_abi(X, Y, c["k"], 0.07, 1.0, g, flags=off)
+    U1, g1 = _fwd_bwd_c_abi(X, Y, c["k"], 0.07, 1.0, g, flags=off, bwd_flags=0, ws_fill=0)
     np.testing.assert_array_equal(U0, U1)
     np.testing.assert_array_equal(g0, g1)
 

@@ -122,6 +122,9 @@ def test_eps_and_problem_mapping():
     assert G._eps_value(1) == 1.0
     with pytest.warns(UserWarning):
         assert G._eps_value(0.0) > 0.0
+    # GLL.py:233-234 use eps only as eps[rows] * eps[cols]: a negative eps is |eps| + the warning
+    with pytest.warns(UserWarning):
+        assert G._eps_value(-0.5) == 0.5
     with pytest.raises(ValueError):
         G._eps_value("bogus")
     p = G.make_problem(8, 4, 3, 2, k=25)
