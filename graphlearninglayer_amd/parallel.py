@@ -16,15 +16,17 @@ def shard_rank_seed(base_seed: int, rank: int) -> int:
     return int(base_seed) + int(rank)
 
 
-def gather_predictions(U: torch.Tensor, group=None, async_op: bool = True):
+def gather_predictions(U: torch.Tensor, group=None, async_op: bool = True,
+                       min_world: int = 2):
     """All-gather every rank's predictions into one (world * m) x C tensor.
 
     Returns (out, work): `out` is filled once `work.wait()` returns (work is None when
-    async_op is False or the world has one rank)."""
+    async_op is False or the world has fewer than `min_world` ranks; `min_world=1` runs the
+    collective even for one rank -- tests use it to drive RCCL on a one-GPU box)."""
     if not dist.is_available() or not dist.is_initialized():
         return U, None
     world = dist.get_world_size(group)
-    if world == 1:
+    if world < min_world:
         return U, None
     U = U.contiguous()
     out = torch.empty((world * U.shape[0],) + tuple(U.shape[1:]), dtype=U.dtype, device=U.device)
@@ -43,13 +45,15 @@ class PredictionGatherer:
     is gathered); the `every`-th call issues ONE asynchronous all_gather_into_tensor of the
     block; `flush()` issues it for a partial group.  Completed groups land in
     `self.gathered` as (world, calls, m, C) tensors in call order once `wait()` returns
-    (only the newest `keep` of them when `keep` is set).  With one rank (or no process
-    group) it is a no-op that records nothing."""
+    (only the newest `keep` of them when `keep` is set).  With fewer than `min_world` ranks
+    (default 2; or no process group) it is a no-op that records nothing: `min_world=1` runs
+    the collective at world size 1 (tests drive RCCL on a one-GPU box that way)."""
 
-    def __init__(self, every: int = 8, group=None, keep=None):
+    def __init__(self, every: int = 8, group=None, keep=None, min_world: int = 2):
         self.every = max(1, int(every))
         self.group = group
         self.keep = keep
+        self.min_world = max(1, int(min_world))
         self._block = None      # (every, m, C) snapshots of the current group
         self._fill = 0
         self.inflight = []      # (out tensor, work)
@@ -61,7 +65,7 @@ class PredictionGatherer:
 
     def _active(self) -> bool:
         return (dist.is_available() and dist.is_initialized()
-                and dist.get_world_size(self.group) > 1)
+                and dist.get_world_size(self.group) >= self.min_world)
 
     def add(self, U: torch.Tensor) -> None:
         if not self._active():

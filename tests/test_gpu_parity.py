@@ -1283,3 +1283,86 @@ def test_select_forms_agree_bitwise(k, d):
     for key in outs[0]:
         np.testing.assert_array_equal(outs[0][key], outs[1][key])
     assert _exact_knn_rows(X, outs[0]["knn_idx"], k) == []
+
+
+# ----------------------------------------------------------------------------------------
+# Class counts other than 10.  The reference takes any label_matrix.shape[1] (GLL.py:32,85),
+# and utils.one_hot_encode(..., 'auto') (utils.py:556-568) yields whatever C the labels have.
+# C = 10 runs the specialised forms (the fused backward, the register-form coefficient);
+# these cases reach the edge-coefficient instantiations (grad.hip launch_backward_grad: exact
+# even C, the 4 / 8 / 16 bounds and the generic loop), the generic-C gradient and the
+# two-launch backward.
+# ----------------------------------------------------------------------------------------
+def _classes_case(C, eps, seed, base=500, batch=500, d=512, k=10):
+    from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
+    X, lab = synth(base, batch, d, C=C, r=1.0, seed=seed)
+    return X, one_hot(lab[:base], C), seeded_gbar(batch, C, seed + 1)
+
+
+@pytest.mark.parametrize("C", [2, 3, 16, 17, 100])
+@pytest.mark.parametrize("eps", [1.0, "auto"])
+def test_class_counts_match_oracle(C, eps):
+    """NS shape (500 + 500 x 512, k = 10), C classes: U and grad_X through apply against the
+    float64 oracle on the GPU's own kNN lists (GLL.py:14-177)."""
+    X, Y, g = _classes_case(C, eps, seed=40 + C)
+    U, gx = _run(X, Y, 0.07, eps, 10, g)
+    assert U.shape == (500, C)
+    ind = _gpu_knn(X, 10, eps)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, st = O.forward(X, Y, tau=0.07, epsilon=eps, K=10, knn=(ind, None))
+    assert O.rel_err(U, Uo) <= TOL
+    assert O.rel_err(gx, O.backward(st, g)) <= TOL
+
+
+@pytest.mark.parametrize("C,eps,shape", [(3, 1.0, "fullysup"), (16, "auto", "fullysup"),
+                                         (17, "auto", "ns"), (6, 1.0, "ns")])
+def test_class_counts_batched_match_oracle(C, eps, shape):
+    """The batched entry at C != 10: FullySup-shape batches take the feature-chunked gradient
+    with the per-edge coefficient pass (edge_coef_kernel<4>/<-16>), NS batches the whole-row
+    gradient's generic-C form; every graph against the oracle."""
+    from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth
+    GLL = _gll()
+    c = CONFIGS[shape]
+    B = 2
+    Xs, Ys, Gs = [], [], []
+    for g_ in range(B):
+        X, lab = synth(c["base"], c["batch"], c["d"], C=C, r=c["r"], seed=60 + g_)
+        Xs.append(X)
+        Ys.append(one_hot(lab[: c["base"]], C))
+        Gs.append(seeded_gbar(c["batch"], C, 70 + g_))
+    Xb = torch.from_numpy(np.stack(Xs)).cuda().requires_grad_(True)
+    Ub = GLL.LaplaceLearningSparseHard.apply(Xb, torch.from_numpy(np.stack(Ys)).cuda(), 0.07, eps,
+                                             c["k"])
+    Ub.backward(torch.from_numpy(np.stack(Gs)).cuda())
+    for g_ in range(B):
+        ind = _gpu_knn(Xs[g_], c["k"], eps)["knn_idx"].cpu().numpy().astype(np.int64)
+        Uo, st = O.forward(Xs[g_], Ys[g_], tau=0.07, epsilon=eps, K=c["k"], knn=(ind, None))
+        assert O.rel_err(Ub[g_].detach().cpu().numpy(), Uo) <= TOL
+        assert O.rel_err(Xb.grad[g_].cpu().numpy(), O.backward(st, Gs[g_])) <= TOL
+
+
+def test_class_count_past_the_grid_cg_large_single_graph():
+    """A single graph with m > 2048 and C = 17: the whole-GPU CG holds C <= 16, so the solves
+    take the per-column kernels; U and grad_X against the oracle."""
+    X, Y, g = _classes_case(17, 1.0, seed=81, base=500, batch=2500, d=64, k=10)
+    U, gx = _run(X, Y, 0.07, 1.0, 10, g)
+    ind = _gpu_knn(X, 10, 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, st = O.forward(X, Y, tau=0.07, epsilon=1.0, K=10, knn=(ind, None))
+    assert O.rel_err(U, Uo) <= TOL
+    assert O.rel_err(gx, O.backward(st, g)) <= TOL
+
+
+@pytest.mark.parametrize("C,nu", [(3, 2750), (17, 2750)])
+def test_utils_laplace_auto_class_count(C, nu):
+    """utils.laplace with n_classes = 'auto' on labels of C classes (utils.py:556-568,570-593):
+    the one-hot width follows the labels, the CSR solve (gll_cg_csr: the whole-GPU CG for
+    C <= 16, per-column kernels past it) against the oracle."""
+    from graphlearninglayer_amd import utils as U_
+    from graphlearninglayer_amd.synth import synth
+    X, labels = synth(250, nu, 64, C=C, r=1.0, seed=90 + C)
+    train = labels[:250]
+    U = U_.laplace(X, train, knn_num=20, epsilon=1.0, tau=1e-8)
+    assert U.shape == (nu, C)
+    ind = _gpu_knn(X, 20, 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo = O.laplace(X, train, knn_num=20, epsilon=1.0, tau=1e-8, knn=(ind, None))
+    assert Uo.shape == (nu, C)
+    assert O.rel_err(U, Uo) <= TOL
