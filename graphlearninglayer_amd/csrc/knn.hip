@@ -1680,6 +1680,362 @@ void knn_select_kernel(
 }
 
 // --------------------------------------------------------------------------------------
+// Wide kNN select (kMaxKm1 < K - 1 <= kMaxKm1Wide: k up to 129 incl. self, e.g. utils.laplace
+// with knn_num = 64 or 100, utils.py:574).  knn_select_kernel holds one candidate per lane, so
+// its list (K - 1 plus a re-rank margin) and the rescan's lanes cap K - 1 at 56.  Here a wave
+// keeps its row's candidates in LDS (kWideCap slots) and its running K - 1 nearest as a sorted
+// list in LDS, and ranks in float64 throughout:
+//   1. the same threshold scan (per-lane TOP = 4 smallest Gram D2 bits, bisection for T with at
+//      least kc = K - 1 + 8 list entries <= T, then every column <= T compacted into LDS; more
+//      than kWideCap ties: T' = the kc-th smallest of the whole row by bisection on full-row
+//      counts, ties at T' in index order);
+//   2. trimming by the Gram error bound (knn_select_kernel step 2b): G = the (K-1)-th smallest
+//      candidate Gram D2, candidates above G + 2B join the left-out bound tb;
+//   3. exact float64 difference-form distances of the kept candidates, 64 per chunk, merged into
+//      the sorted list by (d^2, index) -- the reference's stand-in ranks in float64;
+//   4. the certificate of knn_select_kernel step 5; if it fails, every column with Gram D2 under
+//      the bound is streamed through the same merge (GLL_ST_KNN_RESCAN).
+// Exact for any input like the narrow kernel; distances are the float64 sums rounded once.
+// --------------------------------------------------------------------------------------
+constexpr int kWideCap = 256;   // candidate slots per row
+constexpr int kWideTop = 4;     // per-lane list entries of the threshold scan (64 x 4 >= kc)
+
+struct WideLists {
+    int cj[kWideCap];          // candidates: column
+    uint32_t cg[kWideCap];     // candidates: Gram D2 bits
+    double cd[kWave];          // a chunk's float64 distances
+    int bj[2][kMaxKm1Wide];    // sorted K - 1 nearest (double-buffered merge)
+    double bd[2][kMaxKm1Wide];
+};
+
+// Merge a chunk (lanes < cnt hold candidate cj) into the sorted list `cur` of nb entries:
+// float64 distances, then every entry's rank in the union by (d^2, index); the first K - 1 go
+// to the other buffer.  Returns the new length.  Deterministic (a strict total order).
+template <bool VEC>
+__device__ __forceinline__ int wide_absorb(const float* __restrict__ X, const float* __restrict__ xi,
+                                           int i, int d, int Km1, int cj, int cnt, WideLists& w,
+                                           int& cur, int nb) {
+    const int lane = lane_id();
+    double dv = exact_d2<VEC, 1, double, 4>(X, xi, i, d, lane < cnt ? cj : -1, 0, cnt,
+                                            __builtin_inf());
+    if (!(dv == dv) || lane >= cnt || cj < 0) dv = __builtin_inf();   // NaN rows rank last
+    const int jj = lane < cnt ? cj : INT_MAX;
+    w.cd[lane] = dv;
+    w.cj[lane] = jj;   // the chunk's candidates were read out of cj[] before this call
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const int nxt = cur ^ 1;
+    auto less = [](double da, int ja, double db, int jb) {
+        return da < db || (da == db && ja < jb);
+    };
+    // chunk entry `lane`: its rank among the chunk and among the list
+    int rk = 0;
+    for (int u = 0; u < cnt; ++u) rk += less(w.cd[u], w.cj[u], dv, jj) ? 1 : 0;
+    for (int e = 0; e < nb; ++e) rk += less(w.bd[cur][e], w.bj[cur][e], dv, jj) ? 1 : 0;
+    // list entries: rank = own position + chunk entries before it
+    for (int e0 = 0; e0 < nb; e0 += kWave) {
+        const int e = e0 + lane;
+        if (e < nb) {
+            const double de = w.bd[cur][e];
+            const int je = w.bj[cur][e];
+            int r = e;
+            for (int u = 0; u < cnt; ++u) r += less(w.cd[u], w.cj[u], de, je) ? 1 : 0;
+            if (r < Km1) {
+                w.bd[nxt][r] = de;
+                w.bj[nxt][r] = je;
+            }
+        }
+    }
+    if (lane < cnt && rk < Km1 && dv < __builtin_inf()) {
+        w.bd[nxt][rk] = dv;
+        w.bj[nxt][rk] = jj;
+    }
+    int valid = __popcll(__ballot(lane < cnt && dv < __builtin_inf()));
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    cur = nxt;
+    return min(nb + valid, Km1);
+}
+
+template <bool VEC, int NP>
+__global__ __launch_bounds__(256) void knn_select_wide_kernel(
+    const float* __restrict__ D2, int ld, size_t plane, const float* __restrict__ X, int n, int d,
+    int K, int kc, float eps_fixed, int auto_eps, int RCAP, int32_t* __restrict__ knn_idx,
+    float* __restrict__ knn_d2, float* __restrict__ eps, int32_t* __restrict__ rev_cnt,
+    int32_t* __restrict__ rev_idx, float* __restrict__ rev_d2, int32_t* __restrict__ ovf,
+    int32_t* __restrict__ status, int32_t* __restrict__ status_pub, size_t xs, size_t wss,
+    size_t sts, int r0, int r1, const int32_t* __restrict__ perm) {
+    const int2 gxy = batch_xy<false>();
+    D2 = gshift_at(D2, wss, gxy.y);
+    X = gshift_at(X, xs, gxy.y);
+    knn_idx = gshift_at(knn_idx, wss, gxy.y);
+    knn_d2 = gshift_at(knn_d2, wss, gxy.y);
+    eps = gshift_at(eps, wss, gxy.y);
+    rev_cnt = gshift_at(rev_cnt, wss, gxy.y);
+    rev_idx = gshift_at(rev_idx, wss, gxy.y);
+    rev_d2 = gshift_at(rev_d2, wss, gxy.y);
+    ovf = gshift_at(ovf, wss, gxy.y);
+    status = gshift_at(status, wss, gxy.y);
+    status_pub = gshift_at(status_pub, sts, gxy.y);
+    __shared__ WideLists s_w[4];
+    const int lane = lane_id();
+    const int wv = threadIdx.x >> 6;
+    int i;
+    if (perm) {
+        const int sl = xcd_tile(int(blockIdx.x), int(gridDim.x)) * 4 + wv;
+        if (sl >= r1) return;   // whole wave
+        i = perm[sl];
+    } else {
+        i = r0 + gxy.x * 4 + wv;
+        if (i >= r1) return;    // whole wave
+    }
+    WideLists& w = s_w[wv];
+    const int Km1 = K - 1;
+    const D2Row<false> row{reinterpret_cast<const char*>(D2) + size_t(i - r0) * ld * 4, 1.f};
+    auto bits_of = [&](float x, int j) -> uint32_t {   // invalid: 0xFFFFFFFF (> any T)
+        return (j < n && j != i && x == x) ? __float_as_uint(x > 0.f ? x : 0.f) : 0xFFFFFFFFu;
+    };
+    auto load4 = [&](int jb) {   // columns jb + 4 lane .. + 3 (sum of NP planes), clamped
+        const int j0 = jb + 4 * lane;
+        const int jc = j0 < ld ? j0 : 0;
+        f32x4 v = row.ld4(jc);
+#pragma unroll
+        for (int p = 1; p < NP; ++p) v += row.ld4(p * plane + jc);
+        return v;
+    };
+    auto ld1 = [&](int j) {
+        float x = row.ld1(j);
+#pragma unroll
+        for (int p = 1; p < NP; ++p) x += row.ld1(p * plane + j);
+        return x;
+    };
+    // ---- 1. threshold scan: per-lane TOP smallest bits
+    uint32_t m[kWideTop];
+#pragma unroll
+    for (int t = 0; t < kWideTop; ++t) m[t] = 0xFFFFFFFFu;
+    int nvalid = 0;
+    for (int jb = 0; jb < n; jb += 4 * kWave) {
+        const f32x4 v = load4(jb);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            uint32_t u = bits_of(v[t], jb + 4 * lane + t);
+            nvalid += u != 0xFFFFFFFFu ? 1 : 0;
+#pragma unroll
+            for (int s = 0; s < kWideTop; ++s) {
+                const uint32_t lo = m[s] < u ? m[s] : u;
+                u = m[s] < u ? u : m[s];
+                m[s] = lo;
+            }
+        }
+    }
+    auto count_le = [&](uint32_t t) {
+        int c = 0;
+#pragma unroll
+        for (int s = 0; s < kWideTop; ++s) c += __popcll(__ballot(m[s] <= t));
+        return c;
+    };
+    uint32_t T = 0xFFFFFFFEu;   // fewer than kc valid entries: every valid column
+    if (count_le(T) >= kc) {
+        uint32_t lo = wave_min_u32(m[0]), up = 0;
+        uint32_t top = 0;
+#pragma unroll
+        for (int s = 0; s < kWideTop; ++s) top = m[s] != 0xFFFFFFFFu ? m[s] : top;
+        up = wave_max_u32(top);
+        while (lo < up) {
+            const uint32_t mid = lo + ((up - lo) >> 1);
+            const int c = count_le(mid);
+            if (c == kc) {
+                up = mid;
+                break;
+            }
+            if (c > kc) up = mid;
+            else lo = mid + 1u;
+        }
+        T = up;
+    }
+    // compaction of every column <= T
+    int base = 0, mine = 0;
+    for (int jb = 0; jb < n; jb += 4 * kWave) {
+        const f32x4 v = load4(jb);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int j = jb + 4 * lane + t;
+            const uint32_t u = bits_of(v[t], j);
+            const bool p = u <= T;
+            const uint64_t mk = __ballot(p);
+            const int pos = base + lanes_below(mk);
+            if (p && pos < kWideCap) {
+                w.cj[pos] = j;
+                w.cg[pos] = u;
+            }
+            mine += p ? 1 : 0;
+            base += __popcll(mk);
+        }
+    }
+    uint32_t tb;   // Gram D2 bits every left-out column is >= to
+    int N;
+    if (base > kWideCap) {   // ties: T' = the kc-th smallest of the row, ties in index order
+        if (lane == 0) atomicAdd(&status_pub[GLL_ST_KNN_MERGE], 1);
+        auto count_full = [&](uint32_t thr) {
+            int c = 0;
+            for (int jb = 0; jb < n; jb += 4 * kWave) {
+                const f32x4 v = load4(jb);
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    c += __popcll(__ballot(bits_of(v[t], jb + 4 * lane + t) <= thr));
+            }
+            return c;
+        };
+        uint32_t lo = 0u, up = T;
+        while (lo < up) {
+            const uint32_t mid = lo + ((up - lo) >> 1);
+            if (count_full(mid) >= kc) up = mid;
+            else lo = mid + 1u;
+        }
+        const uint32_t T2 = up;
+        base = 0;
+        for (int pass = 0; pass < 2; ++pass) {   // below T2 (< kc of them), then ties in order
+            for (int j0 = 0; j0 < n && base < kWideCap; j0 += kWave) {
+                const int j = j0 + lane;
+                const uint32_t u = bits_of(j < n ? ld1(j) : 0.f, j);
+                const bool p = pass == 0 ? u < T2 : u == T2;
+                const uint64_t mk = __ballot(p);
+                const int pos = base + lanes_below(mk);
+                if (p && pos < kWideCap) {
+                    w.cj[pos] = j;
+                    w.cg[pos] = u;
+                }
+                base += __popcll(mk);
+            }
+        }
+        N = min(base, kWideCap);
+        tb = T2;
+    } else {
+        N = base;
+        tb = __ballot(mine != nvalid) == 0 ? 0x7F800000u : T + 1u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const float* xi = X + size_t(i) * d;
+    float a2 = ld1(0);   // |a_i|^2: column 0 is the Gram's centre row (a_0 = 0)
+    const double ai = sqrt(double(a2 > 0.f ? a2 : 0.f));
+    // ---- 2. trimming: G = the (K-1)-th smallest candidate Gram D2
+    if (N > Km1) {
+        uint32_t g[kWideCap / kWave];
+#pragma unroll
+        for (int t = 0; t < kWideCap / kWave; ++t) {
+            const int e = t * kWave + lane;
+            g[t] = e < N ? w.cg[e] : 0xFFFFFFFFu;
+        }
+        auto cnt_le = [&](uint32_t thr) {
+            int c = 0;
+#pragma unroll
+            for (int t = 0; t < kWideCap / kWave; ++t) c += __popcll(__ballot(g[t] <= thr));
+            return c;
+        };
+        uint32_t lo = 0u, up = 0xFFFFFFFEu;
+        while (lo < up) {
+            const uint32_t mid = lo + ((up - lo) >> 1);
+            if (cnt_le(mid) >= Km1) up = mid;
+            else lo = mid + 1u;
+        }
+        const double G = double(__uint_as_float(up));
+        const double b0 = kGramErr * (2.0 * ai + sqrt(G)) * (2.0 * ai + sqrt(G));
+        const double rr = 2.0 * ai + sqrt(G + b0);
+        const double thr = G + 2.0 * kGramErr * rr * rr;
+        int keep = 0;
+        uint32_t dmin = 0xFFFFFFFFu;
+#pragma unroll
+        for (int t = 0; t < kWideCap / kWave; ++t) {   // in place: chunk t is read before written
+            const int e = t * kWave + lane;
+            const int j = e < N ? w.cj[e] : -1;
+            const bool live = e < N;
+            const bool need = live && double(__uint_as_float(g[t])) <= thr;
+            if (live && !need) dmin = dmin < g[t] ? dmin : g[t];
+            const uint64_t mk = __ballot(need);
+            if (need) {
+                w.cj[keep + lanes_below(mk)] = j;
+                w.cg[keep + lanes_below(mk)] = g[t];
+            }
+            keep += __popcll(mk);
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+        }
+        dmin = wave_min_u32(dmin);
+        if (dmin < tb) tb = dmin;
+        N = keep;
+    }
+    // ---- 3. float64 distances, merged into the sorted list
+    int cur = 0, nb = 0;
+    for (int c0 = 0; c0 < N; c0 += kWave) {
+        const int cnt = min(kWave, N - c0);
+        const int cj = lane < cnt ? w.cj[c0 + lane] : -1;
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        nb = wide_absorb<VEC>(X, xi, i, d, Km1, cj, cnt, w, cur, nb);
+    }
+    // ---- 4. certificate (knn_select_kernel step 5), else a rescan under the bound
+    if (Km1 >= 1 && nb == Km1 && tb < 0x7F800000u) {
+        const double dK = w.bd[cur][Km1 - 1];
+        const double r = 2.0 * ai + sqrt(dK);
+        const double thr = dK + kGramErr * r * r;
+        if (!(double(__uint_as_float(tb)) > thr)) {
+            if (lane == 0) atomicAdd(&status_pub[GLL_ST_KNN_RESCAN], 1);
+            nb = 0;
+            for (int j0 = 0; j0 < n; j0 += kWave) {
+                const int j = j0 + lane;
+                const float v = j < n ? ld1(j) : 0.f;
+                const bool take = j < n && j != i && v == v && double(v) <= thr;
+                const uint64_t mk = __ballot(take);
+                if (mk == 0ull) continue;
+                if (take) w.cj[lanes_below(mk)] = j;
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+                const int cnt = __popcll(mk);
+                const int cj = lane < cnt ? w.cj[lane] : -1;
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+                nb = wide_absorb<VEC>(X, xi, i, d, Km1, cj, cnt, w, cur, nb);
+            }
+        }
+    }
+    // ---- outputs (knn_select_kernel's)
+    int32_t* oi = knn_idx + size_t(i) * K;
+    float* od = knn_d2 + size_t(i) * K;
+    if (lane == 0) {
+        oi[0] = i;
+        od[0] = 0.f;
+    }
+    for (int r = lane; r < Km1; r += kWave) {
+        const bool live = r < nb;
+        oi[1 + r] = live ? w.bj[cur][r] : i;   // fewer valid: self at 0 (dropped edges)
+        od[1 + r] = live ? float(w.bd[cur][r]) : 0.f;
+    }
+    float ei = eps_fixed;
+    if (auto_eps) ei = nb == Km1 ? sqrtf(float(w.bd[cur][Km1 - 1])) : 0.f;   // GLL.py:205
+    if (lane == 0) {
+        eps[i] = ei;
+        if (!(ei >= 1e-10f)) atomicOr(&status_pub[GLL_ST_TINY_EPS], 1);   // GLL.py:240-241
+    }
+    for (int r = lane; r < nb; r += kWave) {   // reverse entries (ci, i); zero distances dropped
+        const int ci = w.bj[cur][r];
+        const float cef = float(w.bd[cur][r]);
+        if (cef > 0.f) {
+            const int pos = atomicAdd(&rev_cnt[ci], 1);
+            if (pos < RCAP) {
+                rev_idx[size_t(ci) * RCAP + pos] = i;
+                rev_d2[size_t(ci) * RCAP + pos] = cef;
+            } else {
+                const int q = atomicAdd(&status[kStOvfCount], 1);
+                ovf[3 * q + 0] = ci;
+                ovf[3 * q + 1] = i;
+                ovf[3 * q + 2] = __float_as_int(cef);
+            }
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------------
 // gram_pk2_kernel (round 3): the pre-split bf16 GEMM on 256 x 256 upper-triangle tiles with 8
 // waves -- two per SIMD -- of 64 x 128 (2 x 4 accumulators of 32 x 32), k-stages of 32 features.
 // gram_pk_kernel's 128-tile moves 64 KiB into the CU per 48 MFMAs per wave at one wave per
@@ -1944,8 +2300,10 @@ static bool presplit_route(const Layout& L, const Batch& bt) {
 }
 // Batches only (single graphs measured slower with it: at stress the wider candidate margin
 // cost the select 274 -> 299 us; DESIGN.md §3.1, profiles/r03x_d2_fp16_ab.txt).
+// (Not for the wide select, K - 1 > kMaxKm1: it reads fp32 rows.)
 static bool d2_half(const Layout& L, const Batch& bt) {
-    return !(L.flags & GLL_FLAG_D2_F32) && bt.B > 1 && presplit_route(L, bt);
+    return !(L.flags & GLL_FLAG_D2_F32) && bt.B > 1 && presplit_route(L, bt) &&
+           L.K - 1 <= kMaxKm1;
 }
 
 // --------------------------------------------------------------------------------------
@@ -2225,7 +2583,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     // candidate list capacity: smallest of {16, 32, 64} leaving a re-rank margin >= 4
     const int need = K - 1 + 4;
     const int KC = need <= 16 ? 16 : (need <= 32 ? 32 : 64);
-    if (K - 1 > kMaxKm1) return hipErrorInvalidValue;   // the rescan keeps >= 8 lanes free
+    if (K - 1 > kMaxKm1Wide) return hipErrorInvalidValue;
     int margin = KC - (K - 1);
     if (margin > 8) margin = 8;
     int kc = K - 1 + margin;
@@ -2237,6 +2595,28 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     const float* d2s = L.at<float>(ws, L.d2s);
     const int32_t* perm = (locality_order(L, bt) && r0 == 0 && rows == n)
                               ? L.at<int32_t>(ws, L.perm) : nullptr;
+    if (K - 1 > kMaxKm1) {   // k past one candidate per lane: LDS lists (knn_select_wide_kernel)
+        if (h16) return hipErrorInvalidValue;   // d2_half keeps fp32 rows for it
+        const int kcw = min(K - 1 + 8, n - 1);
+        prof_begin(GLL_K_SELECT, s);
+#define GLL_SELW(V, NPV)                                                                       \
+        launch_k(knn_select_wide_kernel<V, NPV>, grid, 256, 0, s, L.at<float>(ws, L.D2), L.ldD,  \
+                 plane, X, n, L.d, K, kcw, eps_fixed, auto_eps ? 1 : 0, L.RCAP,                \
+                 L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps), \
+                 L.at<int32_t>(ws, L.rev_cnt), L.at<int32_t>(ws, L.rev_idx),                   \
+                 L.at<float>(ws, L.rev_d2), L.at<int32_t>(ws, L.ovf), L.at<int32_t>(ws, L.status), \
+                 status_pub, bt.x, bt.ws, bt.st, r0, r0 + rows, perm)
+        if (vec) {
+            if (planes == 2) GLL_SELW(true, 2);
+            else GLL_SELW(true, 1);
+        } else {
+            if (planes == 2) GLL_SELW(false, 2);
+            else GLL_SELW(false, 1);
+        }
+#undef GLL_SELW
+        prof_end(GLL_K_SELECT, s);
+        return launch_status("knn.hip:launch_select(wide)");
+    }
     // the latency form (PG = 2 candidate groups in flight, NU = 16, ~200 VGPRs: 2 waves per SIMD)
     // for a single graph whose rows fill at most one such round of the chip; larger graphs (and
     // batches) run the occupancy form below.  Stress (n = 8,192): 2,048 workgroups, four rounds

@@ -99,10 +99,13 @@ __device__ __forceinline__ float yval(const TY* Y, int j, int C, int c) {
 // of their first 64 staged entries right after staging, so the loads overlap the sort and the
 // weights; the sums still run in sorted-column order (t_idx maps a sorted slot to its staged
 // entry), so results are unchanged.
-template <bool LDS, bool PRE, typename TY>
+// FH: 64-entry halves of the forward list (K - 1 <= 64 FH): entry 64 h + lane of row i's kNN list
+// sits in lane `lane` of fi[h]; its valid entries are staged half after half.
+template <bool LDS, bool PRE, typename TY, int FH>
 __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict__ Y, int i,
-                                          int start, int fi, float fd, bool fval,
-                                          uint64_t fmask, int nf, int rc, float ei, int pri,
+                                          int start, const int (&fi)[FH], const float (&fd)[FH],
+                                          const bool (&fval)[FH], const uint64_t (&fmask)[FH],
+                                          int nf, int rc, float ei, int pri,
                                           float prd, int* s_col, float* s_d2, int* t_col,
                                           float* t_d2, float* t_w, int* t_idx, float* ybuf) {
     const int lane = lane_id();
@@ -112,13 +115,37 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
     float* od2 = LDS ? t_d2 : a.d2e + start;
     float* ow = LDS ? t_w : a.w + start;
     const int Km1 = a.K - 1;
-    const int fself = fval ? fi : -2;
+    int fself[FH];
+    int fbase[FH];   // staged position of each half's first valid entry
     // forward entries
-    if (fval) {
-        const int p = lanes_below(fmask);
-        scol[p] = fi;
-        sd2[p] = fd;
+#pragma unroll
+    for (int h = 0; h < FH; ++h) {
+        fself[h] = fval[h] ? fi[h] : -2;
+        fbase[h] = h == 0 ? 0 : fbase[h - 1] + __popcll(fmask[h - 1]);
+        if (fval[h]) {
+            const int p = fbase[h] + lanes_below(fmask[h]);
+            scol[p] = fi[h];
+            sd2[p] = fd[h];
+        }
     }
+    // the staged position of forward entry t (a valid one): its half's base + valid entries
+    // before it in that half
+    auto fpos = [&](int t) {
+        int p = 0;
+#pragma unroll
+        for (int h = 0; h < FH; ++h)
+            if ((t >> 6) == h) p = fbase[h] + __popcll(fmask[h] & ((1ull << (t & 63)) - 1ull));
+        return p;
+    };
+    auto fmatch = [&](int ri) {   // the forward entry equal to column ri, or -1
+        int tpos = -1;
+#pragma unroll
+        for (int h = 0; h < FH; ++h) {
+            const int tn = min(Km1 - 64 * h, kWave);
+            for (int t = 0; t < tn; ++t) tpos = (ri == readlane_i(fself[h], t)) ? 64 * h + t : tpos;
+        }
+        return tpos;
+    };
     int L = nf;
     // reverse entries, deduplicated against the forward list (mutual pairs)
     const int nr = min(rc, a.RCAP);
@@ -127,8 +154,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
         const bool live = r < nr;
         const int ri = !live ? -1 : (r0 == 0 ? pri : a.rev_idx[size_t(i) * a.RCAP + r]);
         const float rd = !live ? 0.f : (r0 == 0 ? prd : a.rev_d2[size_t(i) * a.RCAP + r]);
-        int tpos = -1;
-        for (int t = 0; t < Km1; ++t) tpos = (ri == readlane_i(fself, t)) ? t : tpos;
+        const int tpos = fmatch(ri);
         const bool keep = live && tpos < 0;
         const uint64_t mk = __ballot(keep);
         if (keep) {
@@ -138,8 +164,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
         }
         if (live && tpos >= 0) {   // mutual pair: union-max (non-negative float bits order)
             if constexpr (!LDS) __threadfence();
-            const int pt = __popcll(fmask & ((1ull << tpos) - 1ull));
-            atomicMax(reinterpret_cast<unsigned*>(sd2) + pt, __float_as_uint(rd));
+            atomicMax(reinterpret_cast<unsigned*>(sd2) + fpos(tpos), __float_as_uint(rd));
         }
         L += __popcll(mk);
     }
@@ -152,8 +177,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
             const int oj = live ? a.ovf[3 * q] : -1;
             const int oi = live ? a.ovf[3 * q + 1] : -1;
             const float od = live ? __int_as_float(a.ovf[3 * q + 2]) : 0.f;
-            int tpos = -1;
-            for (int t = 0; t < Km1; ++t) tpos = (oi == readlane_i(fself, t)) ? t : tpos;
+            const int tpos = fmatch(oi);
             const bool keep = live && oj == i && tpos < 0;
             const uint64_t mk = __ballot(keep);
             if (keep) {
@@ -163,8 +187,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
             }
             if (live && oj == i && tpos >= 0) {   // mutual pair: union-max
                 if constexpr (!LDS) __threadfence();
-                const int pt = __popcll(fmask & ((1ull << tpos) - 1ull));
-                atomicMax(reinterpret_cast<unsigned*>(sd2) + pt, __float_as_uint(od));
+                atomicMax(reinterpret_cast<unsigned*>(sd2) + fpos(tpos), __float_as_uint(od));
             }
             L += __popcll(mk);
         }
@@ -304,7 +327,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
 
 // PRE: label prefetch (single-graph launches; its 20 KiB of LDS halves the workgroups per CU
 // that batches need: B = 64 NS 72 -> 90 us with it)
-template <typename TY, bool PRE, bool FLAT, bool R = false>
+template <typename TY, bool PRE, bool FLAT, bool R = false, int FH = 1>
 __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __restrict__ Y,
                                                         size_t ys) {
     GLL_TRACE_SCOPE(0);
@@ -330,15 +353,24 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
     if (i == 0 && a.gsync)   // single graphs only (grid_cg_route)
         for (int t = lane; t < kGridSyncWords; t += kWave) a.gsync[t] = 0u;
     const int Km1 = a.K - 1;
-    int fi = -1;
-    float fd = 0.f;
-    if (lane < Km1) {
-        fi = a.knn_idx[size_t(i) * a.K + 1 + lane];
-        fd = a.knn_d2[size_t(i) * a.K + 1 + lane];
+    int fi[FH];
+    float fd[FH];
+    bool fval[FH];
+    uint64_t fmask[FH];
+    int nf = 0;
+#pragma unroll
+    for (int h = 0; h < FH; ++h) {
+        const int t = 64 * h + lane;
+        fi[h] = -1;
+        fd[h] = 0.f;
+        if (t < Km1) {
+            fi[h] = a.knn_idx[size_t(i) * a.K + 1 + t];
+            fd[h] = a.knn_d2[size_t(i) * a.K + 1 + t];
+        }
+        fval[h] = t < Km1 && fd[h] > 0.f && fi[h] != i && fi[h] >= 0 && fi[h] < a.n;
+        fmask[h] = __ballot(fval[h]);
+        nf += __popcll(fmask[h]);
     }
-    const bool fval = lane < Km1 && fd > 0.f && fi != i && fi >= 0 && fi < a.n;
-    const uint64_t fmask = __ballot(fval);
-    const int nf = __popcll(fmask);
     const int rc = a.rev_cnt[i];
     const float ei = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[i];   // issued with the lists
     int pri = -1;   // the first 64 reverse-list slots, speculatively with the kNN list
@@ -355,11 +387,101 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
         start = readlane_i(s0, 0);
     }
     if (lbound <= kStage)
-        build_row<true, PRE, TY>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, ei, pri, prd, s_col[wv],
-                            s_d2[wv], t_col[wv], t_d2[wv], t_w[wv], t_idx[wv], ybuf[wv]);
+        build_row<true, PRE, TY, FH>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, ei, pri, prd,
+                                     s_col[wv], s_d2[wv], t_col[wv], t_d2[wv], t_w[wv], t_idx[wv],
+                                     ybuf[wv]);
     else
-        build_row<false, PRE, TY>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, ei, pri, prd, nullptr,
-                             nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+        build_row<false, PRE, TY, FH>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, ei, pri, prd,
+                                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                      nullptr);
+}
+
+// ---------------------------------------------------------------------------------------
+// Sliced ELL for the batched CG (sell_route, gll_internal.h).  The register-ELL CG gathers
+// each wave's slots up to the longest U row among its 64 rows; in natural order one long row
+// per wave sets that bound (NS: 37 gathers per thread and SpMV for 12.5 real entries, and all
+// 24 slots loaded per row at setup).  Here the rows of a graph are ordered by U-block length,
+// longest first (a stable counting sort: ties keep index order, so the order is deterministic),
+// and each 64-row slice -- one wave of the CG -- stores only its widest row's slots: the CG
+// loads and gathers ~19 slots per thread instead of 37, with coalesced loads.  One workgroup per
+// four slices; each recomputes the order from the 2 KB of U-block lengths.
+// ---------------------------------------------------------------------------------------
+template <int S>
+__global__ __launch_bounds__(256) void ell_pack_kernel(int m, const int32_t* __restrict__ ucnt,
+                                                       const int4* __restrict__ ell,
+                                                       int4* __restrict__ sell,
+                                                       int32_t* __restrict__ sperm,
+                                                       int32_t* __restrict__ swid, size_t wss) {
+    constexpr int NB = S + 2;    // key = S + 1 - min(len, S + 1): longest (past the slots) first
+    constexpr int MC = 8;        // 64-row chunks: sell_route has m <= 512
+    static_assert(NB <= 32, "keys fit half a wave");
+    __shared__ int cnt[MC][32];  // rows per key in each chunk
+    __shared__ int pre[MC][32];  // first position of each (chunk, key)
+    __shared__ int p2u[MC * 64];
+    __shared__ int rlen[MC * 64];
+    const int g = int(blockIdx.y);
+    ucnt = gshift_at(ucnt, wss, g);
+    ell = gshift_at(ell, wss, g);
+    sell = gshift_at(sell, wss, g);
+    sperm = gshift_at(sperm, wss, g);
+    swid = gshift_at(swid, wss, g);
+    const int tid = int(threadIdx.x), lane = lane_id(), wv = tid >> 6;
+    int key[2], rank[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int u = tid + 256 * q;
+        const int len = u < m ? ucnt[u] : 0;
+        rlen[u] = len;
+        p2u[u] = m;   // positions past the rows
+        key[q] = u < m ? S + 1 - min(len, S + 1) : NB;
+        rank[q] = 0;
+        int c = 0;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const uint64_t mk = __ballot(key[q] == b);
+            if (key[q] == b) rank[q] = lanes_below(mk);
+            if (lane == b) c = __popcll(mk);
+        }
+        if (lane < 32) cnt[wv + 4 * q][lane] = c;
+    }
+    __syncthreads();
+    if (wv == 0) {   // lane = key: total over chunks, exclusive scan over keys, then per chunk
+        int tot = 0;
+#pragma unroll
+        for (int c = 0; c < MC; ++c) tot += lane < 32 ? cnt[c][lane] : 0;
+        int incl = tot;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const int t = __shfl_up(incl, off);
+            if (lane >= off) incl += t;
+        }
+        int run = incl - tot;
+#pragma unroll
+        for (int c = 0; c < MC; ++c) {
+            if (lane < 32) {
+                pre[c][lane] = run;
+                run += cnt[c][lane];
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+        if (key[q] < NB) p2u[pre[wv + 4 * q][key[q]] + rank[q]] = tid + 256 * q;
+    __syncthreads();
+    const int k = int(blockIdx.x) * 4 + wv;   // this wave's slice
+    if (k >= (m + 63) / 64) return;
+    const int pos = 64 * k + lane;
+    const int u = p2u[pos];
+    int w = u < m ? min(rlen[u], S) : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) w = max(w, __shfl_xor(w, off));
+    const int W = (w + 3) & ~3;   // the CG gathers in groups of four slots
+    sperm[pos] = u;
+    if (lane == 0) swid[k] = W;
+    for (int s2 = 0; s2 < W / 2; ++s2)
+        sell[(size_t(k) * (S / 2) + s2) * 64 + lane] =
+            u < m ? ell[size_t(s2) * m + u] : int4{0, 0, 0, 0};
 }
 
 hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,
@@ -405,16 +527,26 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     a.gsync = grid_cg_route(L, bt) ? L.at<unsigned>(ws, L.cgv) : nullptr;
     a.wss = bt.ws;
     dim3 grid((L.n + 3) / 4, bt.B);
+    const bool pack = sell_route(L, bt);
     prof_begin(GLL_K_FINALIZE, s);
+    if (pack) prof_span(2);   // the row build's phase includes the sliced-ELL pack
     // Batched launches address the workspace through flat pointers (integer-shifted, so the
     // compiler cannot prove them global): measured faster there (NS B = 64 68 -> 63 us, FullySup
     // B = 64 127 -> 116 us, profiles/r02h_rows_flat_ab.txt), while the single-graph kernel is
     // as fast or faster with global loads (6.5 -> 6.4 us).  XCD-contiguous numbering (R) measured
     // slower here even with the graph index taken once (NS B = 64 62 -> 66 us, FullySup B = 64
     // 116 -> 125 us, profiles/r02h_xcd_ab.txt).
+// (K - 1 > 64: the forward list in two 64-entry halves, FH = 2)
 #define GLL_ROWS(T)                                                                          \
     do {                                                                                     \
-        if (bt.B == 1)                                                                       \
+        if (L.K - 1 > kWave) {                                                               \
+            if (bt.B == 1)                                                                   \
+                launch_k(row_build_kernel<T, true, false, false, 2>, grid, 256, 0, s, a,     \
+                         static_cast<const T*>(Y), bt.y);                                    \
+            else                                                                             \
+                launch_k(row_build_kernel<T, false, true, false, 2>, grid, 256, 0, s, a,     \
+                         static_cast<const T*>(Y), bt.y);                                    \
+        } else if (bt.B == 1)                                                                \
             launch_k(row_build_kernel<T, true, false>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y);  \
         else                                                                                 \
             launch_k(row_build_kernel<T, false, true>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y); \
@@ -424,6 +556,11 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     else if (y_dtype == GLL_DT_I64) GLL_ROWS(int64_t);
     else return hipErrorInvalidValue;
 #undef GLL_ROWS
+    if (pack)
+        launch_k(ell_pack_kernel<24>, dim3(unsigned((L.MS + 3) / 4), bt.B), 256, 0, s, L.m,
+                 static_cast<const int32_t*>(a.ucnt), reinterpret_cast<const int4*>(a.ell),
+                 L.at<int4>(ws, L.sell), L.at<int32_t>(ws, L.sperm), L.at<int32_t>(ws, L.swid),
+                 bt.ws);
     prof_end(GLL_K_FINALIZE, s);
     return launch_status("rows.hip:launch_finalize");
 }

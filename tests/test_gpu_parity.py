@@ -926,7 +926,27 @@ def _fwd_bwd_batched_c_abi(Xs, Ys, k, tau, eps, G, flags=0, ws=None):
                                         gd.data_ptr(), _lib.GLL_DT_F64, gx.data_ptr(), s),
                "gll_backward_batched")
     torch.cuda.synchronize()
-    return U.cpu().numpy(), gx.cpu().numpy()
+    return U.cpu().numpy(), gx.cpu().numpy(), ws, prob
+
+
+def _batched_knn_lists(ws, prob, B):
+    """Each graph's kNN list (n x K int32) read from its block of a batched workspace (the lists
+    the batched select kernel itself wrote), via gll_workspace_view."""
+    import ctypes as ct
+    from graphlearninglayer_amd import _lib
+    lib = _lib.lib()
+    wb = lib.gll_workspace_bytes(ct.byref(prob))
+    out = []
+    for g in range(B):
+        view = _lib.View()
+        base = ws.data_ptr() + g * wb
+        _lib.check(lib.gll_workspace_view(ct.byref(prob), base, ct.byref(view)),
+                   "gll_workspace_view")
+        off = view.knn_idx - ws.data_ptr()
+        cnt = prob.n * prob.K
+        out.append(ws[off: off + 4 * cnt].view(torch.int32).reshape(prob.n, prob.K)
+                   .cpu().numpy().astype(np.int64))
+    return out
 
 
 @pytest.mark.parametrize("d,eps", [(64, 1.0), (256, "auto"), (100, "auto")])
@@ -1001,8 +1021,8 @@ def test_fp16_distance_storage_matches_fp32(cfg, B, scale):
     Xs = (Xs * scale).astype(np.float32)
     G = np.stack([seeded_gbar(c["batch"], 10, 700 + g) for g in range(B)])
     eps = "auto"
-    Uh, gh = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, eps, G)
-    Uf, gf = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, eps, G, flags=_lib.FLAG_D2_F32)
+    Uh, gh = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, eps, G)[:2]
+    Uf, gf = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, eps, G, flags=_lib.FLAG_D2_F32)[:2]
     np.testing.assert_array_equal(Uh, Uf)
     np.testing.assert_array_equal(gh, gf)
     if scale != 1.0:   # one workspace, first a batch at 1/scale of these features, then these
@@ -1010,7 +1030,7 @@ def test_fp16_distance_storage_matches_fp32(cfg, B, scale):
         prob = _gll().make_problem(Xs.shape[1], Xs.shape[2], Ys.shape[1], Ys.shape[2], c["k"], 0.07, eps)
         ws = torch.empty(B * _lib.lib().gll_workspace_bytes(ct.byref(prob)), dtype=torch.uint8, device="cuda")
         _fwd_bwd_batched_c_abi((Xs / scale).astype(np.float32), Ys, c["k"], 0.07, eps, G, ws=ws)
-        Ur, gr = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, eps, G, ws=ws)
+        Ur, gr = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, eps, G, ws=ws)[:2]
         np.testing.assert_array_equal(Ur, Uf)
         np.testing.assert_array_equal(gr, gf)
 
@@ -1023,11 +1043,11 @@ def test_batched_graphs_stay_independent_with_non_finite_and_large_features():
     B = 8
     Xs, Ys, c = _synth_batch("ns", B, seed0=81)
     G = np.stack([seeded_gbar(c["batch"], 10, 900 + g) for g in range(B)])
-    U0, g0 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G)
+    U0, g0 = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G)[:2]
     Xb = Xs.copy()
     Xb[2, 700, :] = np.nan
     Xb[5] *= 1e4
-    U1, g1 = _fwd_bwd_batched_c_abi(Xb, Ys, c["k"], 0.07, 1.0, G)
+    U1, g1 = _fwd_bwd_batched_c_abi(Xb, Ys, c["k"], 0.07, 1.0, G)[:2]
     for g in (0, 1, 3, 4, 6, 7):
         np.testing.assert_array_equal(U1[g], U0[g])
         np.testing.assert_array_equal(g1[g], g0[g])
@@ -1045,11 +1065,15 @@ def test_batched_bench_route_matches_oracle_every_graph():
     B = 64
     Xs, Ys, c = _synth_batch("ns", B, seed0=300)
     G = np.stack([seeded_gbar(c["batch"], 10, 700 + g) for g in range(B)])
-    U, gx = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G)[:2]
+    U, gx, ws, prob = _fwd_bwd_batched_c_abi(Xs, Ys, c["k"], 0.07, 1.0, G)
     assert np.isfinite(U).all() and np.isfinite(gx).all()
+    # the oracle is fed the kNN lists the batched launch wrote (each graph's workspace block),
+    # and those lists are the exact float64 kNN
+    inds = _batched_knn_lists(ws, prob, B)
     worst_u = worst_g = 0.0
     for g in range(B):
-        ind = _gpu_knn(Xs[g], c["k"], 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+        ind = inds[g]
+        assert _exact_knn_rows(Xs[g], ind, c["k"]) == [], g
         Uo, st = O.forward(Xs[g], Ys[g], tau=0.07, epsilon=1.0, K=c["k"], knn=(ind, None))
         worst_u = max(worst_u, O.rel_err(U[g], Uo))
         worst_g = max(worst_g, O.rel_err(gx[g], O.backward(st, G[g])))
@@ -1366,3 +1390,108 @@ def test_utils_laplace_auto_class_count(C, nu):
     Uo = O.laplace(X, train, knn_num=20, epsilon=1.0, tau=1e-8, knn=(ind, None))
     assert Uo.shape == (nu, C)
     assert O.rel_err(U, Uo) <= TOL
+
+
+@pytest.mark.parametrize("m,k,eps", [(333, 10, 1.0), (500, 10, "auto"), (449, 11, 1.0)])
+def test_batched_sliced_ell_cg_matches_oracle(m, k, eps):
+    """The batched 256 x 2 CG (B x C > 256 column workgroups, 256 < m <= 512) reads the sliced
+    ELL that rows.hip ell_pack_kernel writes: rows ordered by U-block length, 64 per slice, each
+    slice as wide as its longest row.  Ragged last slices (m = 333, 449), and in every third graph
+    a hub -- 40 rows placed around one U row, whose U block then passes the 24 register slots (its
+    tail comes from the LDS overflow) -- every such graph's U and grad_X against the float64
+    oracle on its own kNN lists (GLL.py:53,93)."""
+    from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
+    B, base, d = 32, 200, 64
+    Xs, Ys, Gs = [], [], []
+    rng = np.random.default_rng(7)
+    for g in range(B):
+        X, lab = synth(base, m, d, r=1.0, seed=500 + g)
+        if g % 3 == 0:   # a hub: rows 260..299 around row 250 (all U rows)
+            X[260:300] = X[250] + 0.02 * rng.standard_normal((40, d)).astype(np.float32)
+            X[260:300] /= np.linalg.norm(X[260:300], axis=1, keepdims=True)
+        Xs.append(X)
+        Ys.append(one_hot(lab[:base]))
+        Gs.append(seeded_gbar(m, 10, 600 + g))
+    Xs, Ys, G = np.stack(Xs), np.stack(Ys), np.stack(Gs)
+    U, gx, ws, prob = _fwd_bwd_batched_c_abi(Xs, Ys, k, 0.07, eps, G)
+    inds = _batched_knn_lists(ws, prob, B)
+    for g in range(0, B, 3):
+        Uo, st = O.forward(Xs[g], Ys[g], tau=0.07, epsilon=eps, K=k, knn=(inds[g], None))
+        assert O.rel_err(U[g], Uo) <= TOL, g
+        assert O.rel_err(gx[g], O.backward(st, G[g])) <= TOL, g
+
+
+# ----------------------------------------------------------------------------------------
+# k past one candidate per lane (kMaxKm1 = 56 < K - 1 <= 128): knn_select_wide_kernel.  The
+# reference takes any k (the constant at GLL.py:27, knn_num in utils.py:574).
+# ----------------------------------------------------------------------------------------
+@pytest.mark.parametrize("k,eps", [(64, 1.0), (100, "auto"), (129, 1.0)])
+def test_wide_k_exact_knn_and_oracle(k, eps):
+    """NS shape (500 + 500 x 512): the kNN lists are the exact float64 kNN, and U and grad_X
+    match the float64 oracle on them (GLL.py:14-177)."""
+    from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth
+    c = CONFIGS["ns"]
+    X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=31)
+    Y = one_hot(lab[: c["base"]])
+    g = seeded_gbar(c["batch"], 10, 32)
+    ind = _gpu_knn(X, k, eps)["knn_idx"].cpu().numpy()
+    assert ind.shape == (c["base"] + c["batch"], k)
+    assert (ind[:, 0] == np.arange(ind.shape[0])).all()
+    assert _exact_knn_rows(X, ind, k) == []
+    U, gx = _run(X, Y, 0.07, eps, k, g)
+    Uo, st = O.forward(X, Y, 0.07, eps, k, knn=(ind.astype(np.int64), None))
+    assert O.rel_err(U, Uo) <= TOL
+    assert O.rel_err(gx, O.backward(st, g)) <= TOL
+
+
+def test_wide_k_batched_and_rescan():
+    """k = 64 through the batched entry (fp32 distance rows: d2_half keeps them for the wide
+    select) against single calls, and a graph whose row 0 -- the Gram's centre -- is far from
+    the rest, so the certificate fails and the exact rescan under the bound runs: still the
+    exact float64 kNN and the oracle's solve."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
+    GLL = _gll()
+    k, B = 64, 3
+    Xs, Ys, c = _synth_batch("ns", B, seed0=41)
+    G = np.stack([seeded_gbar(c["batch"], 10, 42 + g) for g in range(B)])
+    Xb = torch.from_numpy(Xs).cuda().requires_grad_(True)
+    Ub = GLL.LaplaceLearningSparseHard.apply(Xb, torch.from_numpy(Ys).cuda(), 0.07, 1.0, k)
+    Ub.backward(torch.from_numpy(G).cuda())
+    for g in range(B):
+        U1, gx1 = _run(Xs[g], Ys[g], 0.07, 1.0, k, G[g])
+        assert O.rel_err(Ub[g].detach().cpu().numpy(), U1) <= 1e-5
+        assert O.rel_err(Xb.grad[g].cpu().numpy(), gx1) <= 1e-5
+    X, lab = synth(100, 400, 64, r=1.0, seed=23)
+    X[0] = 300.0 / np.sqrt(64)
+    gg = _gpu_knn(X, 80, "auto")
+    ind = gg["knn_idx"].cpu().numpy()
+    assert int(gg["status"][_lib.ST_KNN_RESCAN].item()) > 100
+    assert _exact_knn_rows(X, ind, 80) == []
+    Y = one_hot(lab[:100])
+    gb = seeded_gbar(400, 10, 5)
+    U, grad = _run(X, Y, 0.07, "auto", 80, gb)
+    Uo, st = O.forward(X, Y, 0.07, "auto", 80, knn=(ind.astype(np.int64), None))
+    assert O.rel_err(U, Uo) < TOL
+    assert O.rel_err(grad, O.backward(st, gb)) < TOL
+
+
+@pytest.mark.parametrize("knn_num", [64, 100])
+def test_utils_laplace_wide_knn_num(knn_num):
+    """utils.laplace with knn_num = 64 / 100 (utils.py:574) on 250 + 4,000 points: exact kNN
+    on sampled rows and the oracle's solution."""
+    from graphlearninglayer_amd import utils as U_
+    from graphlearninglayer_amd.synth import synth
+    X, labels = synth(250, 4000, 64, C=10, r=1.0, seed=50 + knn_num)
+    train = labels[:250]
+    U = U_.laplace(X, train, knn_num=knn_num, epsilon=1.0, tau=1e-8)
+    ind = _gpu_knn(X, knn_num, 1.0)["knn_idx"].cpu().numpy()
+    Uo = O.laplace(X, train, knn_num=knn_num, epsilon=1.0, tau=1e-8,
+                   knn=(ind.astype(np.int64), None))
+    assert O.rel_err(U, Uo) <= TOL
+    rng = np.random.default_rng(1)
+    X64 = X.astype(np.float64)
+    for i in rng.choice(X.shape[0], 48, replace=False):
+        d2 = np.sum((X64 - X64[i]) ** 2, axis=1)
+        order = np.argsort(d2, kind="stable")
+        assert set(ind[i].tolist()) == set(order[:knn_num].tolist()), i

@@ -58,8 +58,10 @@ def test_workspace_bytes_and_validation():
     bad = G.make_problem(1000, 512, 500, 10, 10, 0.07, 1.0)
     bad.K = 1
     assert lib.gll_workspace_bytes(ct.byref(bad)) == 0
-    big_k = G.make_problem(1000, 512, 500, 10, 100, 0.07, 1.0)
-    assert lib.gll_workspace_bytes(ct.byref(big_k)) == 0   # K - 1 > 56 (kMaxKm1) unsupported
+    wide_k = G.make_problem(1000, 512, 500, 10, 100, 0.07, 1.0)
+    assert lib.gll_workspace_bytes(ct.byref(wide_k)) > nb   # the wide select (K - 1 <= 128)
+    big_k = G.make_problem(1000, 512, 500, 10, 130, 0.07, 1.0)
+    assert lib.gll_workspace_bytes(ct.byref(big_k)) == 0   # K - 1 > 128 (kMaxKm1Wide) unsupported
     assert lib.gll_strerror(-2).decode().startswith("unsupported")
 
 
@@ -170,17 +172,17 @@ def test_torch_extension_module_loads():
 
 
 def test_k_outside_the_supported_range_raises_a_clear_error():
-    """k (neighbours incl. self) must satisfy 2 <= min(k, n) <= 57 (include/gll.h): the Python
+    """k (neighbours incl. self) must satisfy 2 <= min(k, n) <= 129 (include/gll.h): the Python
     layer says so before anything reaches the device."""
     import torch
     from graphlearninglayer_amd import GLL
-    X = torch.zeros(100, 8)
+    X = torch.zeros(200, 8)
     Y = torch.zeros(10, 3)
-    for k in (1, 58, 100):
+    for k in (1, 130, 150):
         with pytest.raises(ValueError, match="2 <= min"):
             GLL.LaplaceLearningSparseHard.apply(X, Y, 0.0, 1.0, k)
     with pytest.raises(ValueError, match="2 <= min"):
-        GLL.device_graph(X, 64)
+        GLL.device_graph(X, 140)
 
 
 def test_product_library_reads_no_switch_but_debug():
