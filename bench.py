@@ -70,6 +70,11 @@ def parse():
                     help="diagnostic: every rank on cuda:0 over gloo (RCCL refuses two ranks on "
                          "one GPU), to run the real multi-rank GPU leg on a one-GPU box; the "
                          "JSON line is marked and is no scaling measurement")
+    ap.add_argument("--autograd-thread", default="caller", choices=["caller", "device"],
+                    help="where torch's autograd engine runs the backward: 'caller' = the calling "
+                         "thread (torch.autograd.set_multithreading_enabled(False)), 'device' = "
+                         "the engine's per-device worker thread (torch's default); the other mode "
+                         "is measured too and reported as `autograd_other_thread`")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU stand-in step over gloo instead of the GPU path (launcher and "
                          "gather test; the JSON line is marked dry_run and is no measurement)")
@@ -194,6 +199,8 @@ def pmc_traffic(config, kernel):
 
 
 def _newest_profile(pattern):
+    """The newest committed summary matching `pattern` (profiles/<tag>_<cfg>_..., tags sort by
+    round: tools/prof_session.sh + tools/collect_profiles.sh write them)."""
     import glob
     here = os.path.dirname(os.path.abspath(__file__))
     paths = sorted(glob.glob(os.path.join(here, "profiles", pattern)))
@@ -522,7 +529,15 @@ def main():
         for q in range(_lib.K_COUNT):
             _lib.prof_enable(q, PROF_PERIOD)
 
-    # timed region
+    # timed region (the backward on the thread --autograd-thread names: on a host whose torch
+    # engine hand-off to its device thread costs more than the step's GPU work -- ~40 us per
+    # call on some boxes, profiles/r04a_host_breakdown.txt -- the calling thread keeps the
+    # step GPU-bound; the other mode is timed after the run and reported beside it)
+    mt = torch.autograd.set_multithreading_enabled(a.autograd_thread == "device")
+    mt.__enter__()
+    for _ in range(min(a.warmup, 5)):   # untimed: the first steps in this mode
+        step()
+    gatherer.wait()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -534,6 +549,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    mt.__exit__(None, None, None)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -580,7 +596,8 @@ def main():
                     "traffic": traffic, "work_per_launch": work,
                     "avg_launch_us": round(avg_s * 1e6, 3), "launches": cnt,
                     "cg_iters_fwd_bwd": list(iters),
-                    "gram_mfma_pmc": gram_mfma_pmc(a.config)}
+                    "gram_mfma_pmc": gram_mfma_pmc(a.config),
+                    "rocprof_stats": _newest_profile(f"*_{a.config}_kernel_stats.csv")}
         if dominant == "cg_kernel":
             roofline["definition"] = ("SURVEY §8d SpMV roofline: B_spmv x iterations / CG launch "
                                       "time / 8 TB/s, B_spmv = 8 nnz_off(Luu) + 8 m + 8 m C")
@@ -612,10 +629,36 @@ def main():
         for kn, v in per_kernel.items():
             b_, w_ = units[kn]
             v["algorithmic"] = (f"{w_ / 1e9:.4g} GFLOP" if b_ == "mfma" else f"{w_ / 1e6:.4g} MB")
+            # each kernel against its own roof (SURVEY §8d units over its live launch time): the
+            # Gram on the split-bf16 MFMA roof, everything else on 8 TB/s of HBM
+            t_ = v["us_per_launch"] * 1e-6
+            if t_ > 0:
+                v["roofline_frac"] = round(w_ / t_ / 1e12 / GRAM_ROOF_TFS if b_ == "mfma"
+                                           else w_ / t_ / 1e9 / HBM_PEAK_GBS, 5)
+                pt = pmc_traffic(a.config, kn)
+                if pt:
+                    v["pmc_traffic_over_algorithmic"] = round(pt / w_, 3) if b_ == "hbm" else None
 
     c_abi = None
     if not a.no_profile:
         c_abi = c_abi_measure(X, Y, tau, eps, k, gbar, a.steps, a.warmup)
+
+    # the same step with the autograd engine's other threading mode (labelled, not `value`)
+    other = None
+    if world == 1 and not a.no_profile:
+        with torch.autograd.set_multithreading_enabled(a.autograd_thread != "device"):
+            for _ in range(a.warmup):
+                step()
+            torch.cuda.synchronize()
+            t0_ = time.perf_counter()
+            for _ in range(a.steps):
+                step()
+            torch.cuda.synchronize()
+            el_ = time.perf_counter() - t0_
+        other = {"autograd_thread": "device" if a.autograd_thread != "device" else "caller",
+                 "value": round(a.steps / el_, 3), "unit": "calls/s",
+                 "ms_per_step": round(1e3 * el_ / a.steps, 4),
+                 "note": "the same apply + autograd.grad step with torch's other engine threading"}
 
     # the adversarial scripts' inline-copy call (train_and_adversarial.py:721,745;
     # adversarial.py:534): lap(features, one_hot(labels)[:k]) -- int64 labels, tau = 0, eps =
@@ -697,6 +740,9 @@ def main():
             "gather_check": gather_check,
             "kernels": per_kernel,
             "c_abi": c_abi,
+            "autograd_thread": (a.autograd_thread + (" (torch.autograd.set_multithreading_enabled("
+                                f"{a.autograd_thread == 'device'}))")),
+            "autograd_other_thread": other,
             "batched": batched,
             "auto_eps_extra": auto_extra,
             "gll_env": gll_env,

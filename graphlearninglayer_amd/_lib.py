@@ -29,7 +29,7 @@ FLAG_KNN_PANEL = 65536    # kNN in row panels (O(panel x n) distances)
 FLAG_D2_F32 = 131072      # fp32 distance matrix on the pre-split Gram route
 FLAG_ROW_ORDER_OFF = 262144   # large single graphs: row-index order instead of the locality order
 # process-wide test knobs (gll_set_knob): force a code path, 0 = automatic
-KNOB_VR_RV, KNOB_GRID_CAP, KNOB_GRAM_TILE, KNOB_SEL_FORM, KNOB_GRAM_TAIL = 0, 1, 2, 3, 4
+KNOB_VR_RV, KNOB_GRID_CAP, KNOB_GRAM_TILE, KNOB_SEL_FORM, KNOB_GRAM_TAIL, KNOB_ROW_PRE = 0, 1, 2, 3, 4, 5
 ST_TINY_EPS, ST_FWD_NONCONV, ST_FWD_ITERS, ST_BWD_NONCONV, ST_BWD_ITERS = 0, 1, 2, 3, 4
 ST_KNN_RESCAN = 5   # kNN rows re-ranked over every column under the Gram error bound
 ST_SOLVE_FAILED = 6   # the fused backward gave up on its adjoint solves: grad NaN, raised

@@ -209,12 +209,6 @@ struct Layout {
     size_t d2s;       // float: the fp16 D2 scale of the pre-split GEMM (knn.hip tile_d2_scale)
     size_t pid, perm; // locality order (order_rows): nearest pivot of each row, the row order
     size_t ohist;     // locality order: rows per pivot of each 64-row block ([ceil(n/64)][64])
-    // Sliced ELL of the batched CG (sell_route; rows.hip ell_pack_kernel): the U rows ordered by
-    // U-block length (longest first, stable), 64 per slice = one wave of the CG; slice k keeps
-    // only its widest row's slots, column-major per slice (record (k, s2, lane) at
-    // (k SE/2 + s2) 64 + lane).  sperm: position -> U row (m past the rows); swid: slots per slice.
-    int MS;           // slices: ceil(m / 64)
-    size_t sell, sperm, swid;
 
     explicit Layout(const gll_problem& p) {
         n = p.n; d = p.d; base = p.base; C = p.C;
@@ -270,10 +264,6 @@ struct Layout {
         pid = take(size_t(n) * 4);
         perm = take(size_t(n) * 4);
         ohist = take(size_t((n + 63) / 64) * 64 * 4);
-        MS = (m + 63) / 64;
-        sell = take(size_t(SE / 2) * MS * 64 * 16);
-        sperm = take(size_t(MS) * 64 * 4);
-        swid = take(size_t(MS) * 4);
         P = take(size_t(n) * C * 4);       // [Y; U] as fp32 (backward's P, GLL.py:109)
         Wadj = take(size_t(n) * C * 4);    // [0; Luu^-1 gbar] (backward's w, GLL.py:104)
         S = take(size_t(Etot) * 4);        // per-edge coefficient (auto eps / chunked gradient)
@@ -611,13 +601,6 @@ hipError_t launch_order(const Layout& L, void* ws, hipStream_t s);
 inline bool grid_cg_route(const Layout& L, const Batch& bt) {
     return bt.B == 1 && L.C <= 16 && !(L.flags & GLL_FLAG_CG_PERCOL) &&
            (L.m > 2048 || (L.flags & GLL_FLAG_CG_GRID));
-}
-// The per-column CG of this launch runs the batched 256 x 2 register-ELL geometry (solve.hip
-// cg_dispatch: 256 < m <= 512 and more than 256 column workgroups) and reads the sliced ELL that
-// rows.hip's ell_pack_kernel writes after the row build.  A function of the problem and B only.
-inline bool sell_route(const Layout& L, const Batch& bt) {
-    return L.RV == 0 && L.SE == 24 && L.m > 256 && L.m <= 512 && bt.B > 1 &&
-           int64_t(bt.B) * L.C > 256;
 }
 hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,
                            int y_dtype, float tau, float eps_fixed, hipStream_t s);

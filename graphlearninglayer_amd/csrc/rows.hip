@@ -396,94 +396,6 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
                                       nullptr);
 }
 
-// ---------------------------------------------------------------------------------------
-// Sliced ELL for the batched CG (sell_route, gll_internal.h).  The register-ELL CG gathers
-// each wave's slots up to the longest U row among its 64 rows; in natural order one long row
-// per wave sets that bound (NS: 37 gathers per thread and SpMV for 12.5 real entries, and all
-// 24 slots loaded per row at setup).  Here the rows of a graph are ordered by U-block length,
-// longest first (a stable counting sort: ties keep index order, so the order is deterministic),
-// and each 64-row slice -- one wave of the CG -- stores only its widest row's slots: the CG
-// loads and gathers ~19 slots per thread instead of 37, with coalesced loads.  One workgroup per
-// four slices; each recomputes the order from the 2 KB of U-block lengths.
-// ---------------------------------------------------------------------------------------
-template <int S>
-__global__ __launch_bounds__(256) void ell_pack_kernel(int m, const int32_t* __restrict__ ucnt,
-                                                       const int4* __restrict__ ell,
-                                                       int4* __restrict__ sell,
-                                                       int32_t* __restrict__ sperm,
-                                                       int32_t* __restrict__ swid, size_t wss) {
-    constexpr int NB = S + 2;    // key = S + 1 - min(len, S + 1): longest (past the slots) first
-    constexpr int MC = 8;        // 64-row chunks: sell_route has m <= 512
-    static_assert(NB <= 32, "keys fit half a wave");
-    __shared__ int cnt[MC][32];  // rows per key in each chunk
-    __shared__ int pre[MC][32];  // first position of each (chunk, key)
-    __shared__ int p2u[MC * 64];
-    __shared__ int rlen[MC * 64];
-    const int g = int(blockIdx.y);
-    ucnt = gshift_at(ucnt, wss, g);
-    ell = gshift_at(ell, wss, g);
-    sell = gshift_at(sell, wss, g);
-    sperm = gshift_at(sperm, wss, g);
-    swid = gshift_at(swid, wss, g);
-    const int tid = int(threadIdx.x), lane = lane_id(), wv = tid >> 6;
-    int key[2], rank[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int u = tid + 256 * q;
-        const int len = u < m ? ucnt[u] : 0;
-        rlen[u] = len;
-        p2u[u] = m;   // positions past the rows
-        key[q] = u < m ? S + 1 - min(len, S + 1) : NB;
-        rank[q] = 0;
-        int c = 0;
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const uint64_t mk = __ballot(key[q] == b);
-            if (key[q] == b) rank[q] = lanes_below(mk);
-            if (lane == b) c = __popcll(mk);
-        }
-        if (lane < 32) cnt[wv + 4 * q][lane] = c;
-    }
-    __syncthreads();
-    if (wv == 0) {   // lane = key: total over chunks, exclusive scan over keys, then per chunk
-        int tot = 0;
-#pragma unroll
-        for (int c = 0; c < MC; ++c) tot += lane < 32 ? cnt[c][lane] : 0;
-        int incl = tot;
-#pragma unroll
-        for (int off = 1; off < kWave; off <<= 1) {
-            const int t = __shfl_up(incl, off);
-            if (lane >= off) incl += t;
-        }
-        int run = incl - tot;
-#pragma unroll
-        for (int c = 0; c < MC; ++c) {
-            if (lane < 32) {
-                pre[c][lane] = run;
-                run += cnt[c][lane];
-            }
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-        if (key[q] < NB) p2u[pre[wv + 4 * q][key[q]] + rank[q]] = tid + 256 * q;
-    __syncthreads();
-    const int k = int(blockIdx.x) * 4 + wv;   // this wave's slice
-    if (k >= (m + 63) / 64) return;
-    const int pos = 64 * k + lane;
-    const int u = p2u[pos];
-    int w = u < m ? min(rlen[u], S) : 0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) w = max(w, __shfl_xor(w, off));
-    const int W = (w + 3) & ~3;   // the CG gathers in groups of four slots
-    sperm[pos] = u;
-    if (lane == 0) swid[k] = W;
-    for (int s2 = 0; s2 < W / 2; ++s2)
-        sell[(size_t(k) * (S / 2) + s2) * 64 + lane] =
-            u < m ? ell[size_t(s2) * m + u] : int4{0, 0, 0, 0};
-}
-
 hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,
                            int y_dtype, float tau, float eps_fixed, hipStream_t s) {
     if (L.C > kMaxCPerLane * kWave) return hipErrorInvalidValue;
@@ -527,9 +439,10 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     a.gsync = grid_cg_route(L, bt) ? L.at<unsigned>(ws, L.cgv) : nullptr;
     a.wss = bt.ws;
     dim3 grid((L.n + 3) / 4, bt.B);
-    const bool pack = sell_route(L, bt);
+    // label prefetch: single graphs (its LDS halves the resident workgroups, which batches need)
+    const int kp = knob(GLL_KNOB_ROW_PRE);
+    const bool pre = kp == 1 || (kp == 0 && bt.B == 1);
     prof_begin(GLL_K_FINALIZE, s);
-    if (pack) prof_span(2);   // the row build's phase includes the sliced-ELL pack
     // Batched launches address the workspace through flat pointers (integer-shifted, so the
     // compiler cannot prove them global): measured faster there (NS B = 64 68 -> 63 us, FullySup
     // B = 64 127 -> 116 us, profiles/r02h_rows_flat_ab.txt), while the single-graph kernel is
@@ -546,8 +459,10 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
             else                                                                             \
                 launch_k(row_build_kernel<T, false, true, false, 2>, grid, 256, 0, s, a,     \
                          static_cast<const T*>(Y), bt.y);                                    \
-        } else if (bt.B == 1)                                                                \
+        } else if (pre)                                                                      \
             launch_k(row_build_kernel<T, true, false>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y);  \
+        else if (bt.B == 1)                                                                  \
+            launch_k(row_build_kernel<T, false, false>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y); \
         else                                                                                 \
             launch_k(row_build_kernel<T, false, true>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y); \
     } while (0)
@@ -556,11 +471,6 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     else if (y_dtype == GLL_DT_I64) GLL_ROWS(int64_t);
     else return hipErrorInvalidValue;
 #undef GLL_ROWS
-    if (pack)
-        launch_k(ell_pack_kernel<24>, dim3(unsigned((L.MS + 3) / 4), bt.B), 256, 0, s, L.m,
-                 static_cast<const int32_t*>(a.ucnt), reinterpret_cast<const int4*>(a.ell),
-                 L.at<int4>(ws, L.sell), L.at<int32_t>(ws, L.sperm), L.at<int32_t>(ws, L.swid),
-                 bt.ws);
     prof_end(GLL_K_FINALIZE, s);
     return launch_status("rows.hip:launch_finalize");
 }

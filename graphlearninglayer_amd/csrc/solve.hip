@@ -198,10 +198,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int& total) 
 // non-null: the solution is stored write-through (sc1) and, once every wave has drained its
 // stores, thread 0 adds 1 to fsync[0] -- the feature-gradient workgroups of the same launch
 // wait for C arrivals (the hand-off protocol of DESIGN.md §3.5).
-// SELL: the rows come in rows.hip ell_pack_kernel's length order and the slots from its sliced
-// ELL (sell / sperm / swid, gll_internal.h Layout): position p = tid + NT q holds U row sperm[p],
-// and its wave loads and gathers only the slice's width of slots.
-template <int NT, int R, int S, typename TB, int MODE, bool SELL = false>
+template <int NT, int R, int S, typename TB, int MODE>
 __device__ __forceinline__ void cg_ell_body(
     int2 gxy, unsigned* fsync,
     int m, int C, int base, const int32_t* __restrict__ row_start,
@@ -210,8 +207,7 @@ __device__ __forceinline__ void cg_ell_body(
     const TB* __restrict__ bsrc, double* __restrict__ out64, float* __restrict__ out32,
     float rtol, int max_iter, int mat_cap, int32_t* __restrict__ st_nonconv,
     int32_t* __restrict__ st_iters, const int4* __restrict__ ell, size_t wss, size_t bs,
-    size_t us, size_t sts, const int32_t* __restrict__ sperm = nullptr,
-    const int32_t* __restrict__ swid = nullptr) {
+    size_t us, size_t sts) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     ell = gshift_at(ell, wss, gxy.y);
     row_start = gshift_br_at(row_start, wss, gxy.y);   // batched launches: graph blockIdx.y
@@ -236,25 +232,8 @@ __device__ __forceinline__ void cg_ell_body(
     // (Ordering rows by length so each wave's slot bound tracks its own rows was measured:
     // no gain per iteration at NS, +1.5 us of setup from the permuted ELL loads.)
     int urow[R];   // the row each thread slot handles
-    int wid[R];    // SELL: slots of the slice (wave-uniform)
-    if constexpr (SELL) {
-        sperm = gshift_at(sperm, wss, gxy.y);
-        swid = gshift_at(swid, wss, gxy.y);
-        const int ms = (m + 63) >> 6;
 #pragma unroll
-        for (int q = 0; q < R; ++q) {
-            const int pos = tid + NT * q;
-            const bool in = (pos >> 6) < ms;
-            urow[q] = in ? sperm[pos] : m;
-            wid[q] = __builtin_amdgcn_readfirstlane(in ? swid[pos >> 6] : 0);
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < R; ++q) {
-            urow[q] = tid + NT * q;
-            wid[q] = S;
-        }
-    }
+    for (int q = 0; q < R; ++q) urow[q] = tid + NT * q;
     int ec[R][S];
     float ew[R][S];
     int ost[R], olen[R];
@@ -276,16 +255,7 @@ __device__ __forceinline__ void cg_ell_body(
         static_assert(S % 2 == 0, "two ELL slots per 16-B record");
 #pragma unroll
         for (int s2 = 0; s2 < S / 2; ++s2) {   // column-major ELL records (row_build): coalesced
-            int4 v;
-            if constexpr (SELL) {   // the slice's records only (wave-uniform width)
-                const int pos = tid + NT * q;
-                if (2 * s2 < wid[q])
-                    v = ell[(size_t(pos >> 6) * (S / 2) + s2) * 64 + (pos & 63)];
-                else
-                    v = int4{0, 0, 0, 0};
-            } else {
-                v = ell[size_t(s2) * m + uc];
-            }
+            const int4 v = ell[size_t(s2) * m + uc];
             ec[q][2 * s2] = v.x;
             ew[q][2 * s2] = __int_as_float(v.y);
             ec[q][2 * s2 + 1] = v.z;
@@ -362,8 +332,7 @@ __device__ __forceinline__ void cg_ell_body(
         // in groups of 4: rows average ~6 of the 24 slots at NS).
         int smax[R];
 #pragma unroll
-        for (int q = 0; q < R; ++q)
-            smax[q] = SELL ? wid[q] : wave_max_int(ulen[q] < S ? ulen[q] : S);
+        for (int q = 0; q < R; ++q) smax[q] = wave_max_int(ulen[q] < S ? ulen[q] : S);
         auto spmv = [&](int q, float pq, const float* Pb) {
             float pv[S];
 #pragma unroll
@@ -566,7 +535,7 @@ __device__ __forceinline__ void cg_ell_body(
 
 // The batched geometry (256 x 2, MODE 1: B x C > 256 column workgroups) must keep three
 // workgroups per CU -- B = 64 NS is 640 of them, all resident at once -- so <= 168 VGPRs.
-template <int NT, int R, int S, typename TB, int MODE, bool SELL = false>
+template <int NT, int R, int S, typename TB, int MODE>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 && R == 2 && MODE == 1 ? 3 : 1)))
 void cg_ell_kernel(
     int m, int C, int base, const int32_t* __restrict__ row_start,
@@ -575,12 +544,11 @@ void cg_ell_kernel(
     const TB* __restrict__ bsrc, double* __restrict__ out64, float* __restrict__ out32,
     float rtol, int max_iter, int mat_cap, int32_t* __restrict__ st_nonconv,
     int32_t* __restrict__ st_iters, const int4* __restrict__ ell, size_t wss, size_t bs,
-    size_t us, size_t sts, const int32_t* __restrict__ sperm, const int32_t* __restrict__ swid) {
+    size_t us, size_t sts) {
     // batch_xy once: per pointer it re-reads gridDim and divides
-    cg_ell_body<NT, R, S, TB, MODE, SELL>(batch_xy<true>(), nullptr, m, C, base, row_start,
-                                          row_len, ucnt, col, wv, diag, bsrc, out64, out32, rtol,
-                                          max_iter, mat_cap, st_nonconv, st_iters, ell, wss, bs,
-                                          us, sts, sperm, swid);
+    cg_ell_body<NT, R, S, TB, MODE>(batch_xy<true>(), nullptr, m, C, base, row_start, row_len,
+                                    ucnt, col, wv, diag, bsrc, out64, out32, rtol, max_iter,
+                                    mat_cap, st_nonconv, st_iters, ell, wss, bs, us, sts);
 }
 
 // --------------------------------------------------------------------------------------
@@ -980,7 +948,7 @@ __global__ __launch_bounds__(NT) void cg_lds_kernel(
 }
 
 
-template <int NT, int R, int S, typename TB, int MODE, bool SELL = false>
+template <int NT, int R, int S, typename TB, int MODE>
 static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* b, size_t bs,
                           double* out64, float* out32, float rtol, int max_iter,
                           int32_t* st_nonconv, int32_t* st_iters, hipStream_t s) {
@@ -999,15 +967,13 @@ static hipError_t run_ell(const Layout& L, const Batch& bt, void* ws, const TB* 
     // the kernel holds the first S of the ell_emit(L, B) slots row_build wrote in registers
     // (entries past S come from the CSR through the LDS overflow)
     if (S > ell_emit(L, bt.B)) return hipErrorInvalidValue;
-    auto fn = cg_ell_kernel<NT, R, S, TB, MODE, SELL>;
+    auto fn = cg_ell_kernel<NT, R, S, TB, MODE>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
     launch_k(fn, dim3(L.C, bt.B), NT, lds, s,
         L.m, L.C, L.base, L.at<int32_t>(ws, L.row_start), L.at<int32_t>(ws, L.row_len),
         L.at<int32_t>(ws, L.ucnt), L.at<int32_t>(ws, L.col), L.at<float>(ws, L.w),
         L.at<float>(ws, L.diag), b, out64, out32, rtol, max_iter, int(cap), st_nonconv, st_iters,
-        L.at<int4>(ws, SELL ? L.sell : L.ell), bt.ws, bs, bt.u, bt.st,
-        static_cast<const int32_t*>(L.at<int32_t>(ws, L.sperm)),
-        static_cast<const int32_t*>(L.at<int32_t>(ws, L.swid)));
+        L.at<int4>(ws, L.ell), bt.ws, bs, bt.u, bt.st);
     return launch_status("solve.hip:run_ell");
 }
 
@@ -1367,13 +1333,7 @@ static hipError_t cg_dispatch(const Layout& L, const Batch& bt, void* ws, const 
     // workgroup -- measured slower at B = 64 and 8 and were removed in round 4:
     // profiles/r03s_cg_pairs_ab.txt.)
     if (m <= 512 && (bt.B == 1 || int64_t(bt.B) * L.C <= 256)) GLL_ELL(512, 1, 24);
-    if (m <= 512) {
-        // the sliced ELL of rows.hip ell_pack_kernel (written by the forward's row build)
-        if (sell_route(L, bt))
-            return run_ell<256, 2, 24, TB, 1, true>(L, bt, ws, b, bs, out64, out32, rtol,
-                                                    max_iter, st_nonconv, st_iters, s);
-        GLL_ELL(256, 2, 24);
-    }
+    if (m <= 512) GLL_ELL(256, 2, 24);
     if (m <= 1024) GLL_ELL(1024, 1, 16);
     if (m <= 2048) GLL_ELL(1024, 2, 16);
     if (m <= 4096) GLL_ELL(1024, 4, 4);

@@ -1393,13 +1393,12 @@ def test_utils_laplace_auto_class_count(C, nu):
 
 
 @pytest.mark.parametrize("m,k,eps", [(333, 10, 1.0), (500, 10, "auto"), (449, 11, 1.0)])
-def test_batched_sliced_ell_cg_matches_oracle(m, k, eps):
-    """The batched 256 x 2 CG (B x C > 256 column workgroups, 256 < m <= 512) reads the sliced
-    ELL that rows.hip ell_pack_kernel writes: rows ordered by U-block length, 64 per slice, each
-    slice as wide as its longest row.  Ragged last slices (m = 333, 449), and in every third graph
-    a hub -- 40 rows placed around one U row, whose U block then passes the 24 register slots (its
-    tail comes from the LDS overflow) -- every such graph's U and grad_X against the float64
-    oracle on its own kNN lists (GLL.py:53,93)."""
+def test_batched_two_row_cg_ragged_and_hub_rows_match_oracle(m, k, eps):
+    """The batched 256 x 2 CG (B x C > 256 column workgroups, 256 < m <= 512; solve.hip
+    cg_dispatch) with ragged row counts (m = 333, 449: dead threads in the last waves), and in
+    every third graph a hub -- 40 rows placed around one U row, whose U block then passes the 24
+    register slots (its tail comes from the LDS overflow) -- every such graph's U and grad_X
+    against the float64 oracle on its own kNN lists (GLL.py:53,93)."""
     from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
     B, base, d = 32, 200, 64
     Xs, Ys, Gs = [], [], []
