@@ -218,7 +218,10 @@ struct Layout {
         ldD = (n + 3) & ~3;
         PR = panel_rows(n, flags);
         KS = PR < n ? 1 : gram_splits(n, d);
-        RCAP = 4 * (K - 1) + 8;
+        // reverse-list capacity: past it a row's reverse entries go to the global overflow
+        // list, which each such (hub) row then scans whole -- at stress (K = 30) 4(K-1)+8 left
+        // 39 hubs scanning 742 entries, 14 of their 35 us (profiles/r05w_trace_stress.txt)
+        RCAP = 8 * (K - 1) + 8;
         Wcap = (K - 1) + RCAP;
         Etot = int64_t(n) * Wcap + 2LL * n * (K - 1);
         size_t off = 0;

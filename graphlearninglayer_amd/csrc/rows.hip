@@ -20,6 +20,18 @@ namespace gll {
 
 GLL_TRACE_UNIT(rows)
 
+// Row checkpoints (trace builds): slots 1.. for row `base` (the first unlabeled row), 11.. for a
+// hub row (reverse list past RCAP; the last one to get there), 20 / 21 the longest wave among
+// every 16th row / among the hub rows (s_memrealtime ticks, atomicMax).
+#ifdef GLL_TRACE
+#define GLL_ROW_PT(q)                                                                         \
+    do {                                                                                     \
+        if (lane_id() == 0 && tslot >= 0) g_trace[tslot + (q)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define GLL_ROW_PT(q) do {} while (0)
+#endif
+
 constexpr int kStage = 256;      // per-wave LDS staging capacity (entries)
 constexpr int kMaxCPerLane = 4;  // classes per lane in the rhs accumulation (C <= 256)
 constexpr int kYPre = 16;        // label prefetch: classes held per staged entry (C <= 16)
@@ -107,8 +119,10 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
                                           const bool (&fval)[FH], const uint64_t (&fmask)[FH],
                                           int nf, int rc, float ei, int pri,
                                           float prd, int* s_col, float* s_d2, int* t_col,
-                                          float* t_d2, float* t_w, int* t_idx, float* ybuf) {
+                                          float* t_d2, float* t_w, int* t_idx, float* ybuf,
+                                          int tslot) {
     const int lane = lane_id();
+    (void)tslot;
     int* scol = LDS ? s_col : a.tmp_col + start;
     float* sd2 = LDS ? s_d2 : a.tmp_d2 + start;
     int* ocol = LDS ? t_col : a.col + start;
@@ -168,31 +182,57 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
         }
         L += __popcll(mk);
     }
+    GLL_ROW_PT(9);
     if (rc > a.RCAP) {  // hub row: the remaining reverse entries sit in the overflow list
         const int novf = __hip_atomic_load(&a.status[kStOvfCount], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
-        for (int q0 = 0; q0 < novf; q0 += kWave) {
-            const int q = q0 + lane;
-            const bool live = q < novf;
-            const int oj = live ? a.ovf[3 * q] : -1;
-            const int oi = live ? a.ovf[3 * q + 1] : -1;
-            const float od = live ? __int_as_float(a.ovf[3 * q + 2]) : 0.f;
-            const int tpos = fmatch(oi);
-            const bool keep = live && oj == i && tpos < 0;
-            const uint64_t mk = __ballot(keep);
-            if (keep) {
-                const int p = L + lanes_below(mk);
-                scol[p] = oi;
-                sd2[p] = od;
+        GLL_ROW_PT(8);
+#ifdef GLL_TRACE
+        if (tslot == 10 && lane == 0) g_trace[22] = novf;
+#endif
+        // the whole list is scanned by every hub row: OB chunks of 64 triples are loaded
+        // before any is matched (one memory round trip per 512 entries, not per 64: a stress
+        // hub row spent 22 of its 43 us here, profiles/r05t_trace_stress.txt); entries are
+        // still taken in list order
+        constexpr int OB = 8;
+        for (int q0 = 0; q0 < novf; q0 += OB * kWave) {
+            int ojs[OB], ois[OB];
+            float ods[OB];
+#pragma unroll
+            for (int b = 0; b < OB; ++b) {
+                const int q = q0 + b * kWave + lane;
+                const bool live = q < novf;
+                ojs[b] = live ? a.ovf[3 * q] : -1;
+                ois[b] = live ? a.ovf[3 * q + 1] : -1;
+                ods[b] = live ? __int_as_float(a.ovf[3 * q + 2]) : 0.f;
             }
-            if (live && oj == i && tpos >= 0) {   // mutual pair: union-max
-                if constexpr (!LDS) __threadfence();
-                atomicMax(reinterpret_cast<unsigned*>(sd2) + fpos(tpos), __float_as_uint(od));
+#pragma unroll
+            for (int b = 0; b < OB; ++b) {
+                if (q0 + b * kWave >= novf) break;   // wave-uniform
+                const int oj = ojs[b], oi = ois[b];
+                const float od = ods[b];
+                const bool mine_e = oj == i;   // dead slots hold -1
+                const int tpos = __ballot(mine_e) ? fmatch(oi) : -1;
+                const bool keep = mine_e && tpos < 0;
+                const uint64_t mk = __ballot(keep);
+                if (keep) {
+                    const int p = L + lanes_below(mk);
+                    scol[p] = oi;
+                    sd2[p] = od;
+                }
+                if (mine_e && tpos >= 0) {   // mutual pair: union-max
+                    if constexpr (!LDS) __threadfence();
+                    atomicMax(reinterpret_cast<unsigned*>(sd2) + fpos(tpos), __float_as_uint(od));
+                }
+                L += __popcll(mk);
             }
-            L += __popcll(mk);
+#ifdef GLL_TRACE
+            if (tslot == 10 && lane == 0 && q0 == 0) g_trace[23] = __builtin_amdgcn_s_memrealtime();
+#endif
         }
     }
     if constexpr (!LDS) __threadfence();
+    GLL_ROW_PT(2);
     // label prefetch (unlabeled rows): lane e < 64 loads Y of staged entry e when labeled
     const bool ypre = LDS && PRE && i >= a.base && a.C <= kYPre;
     float yreg[kYPre];
@@ -202,16 +242,41 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
 #pragma unroll
         for (int c = 0; c < kYPre; ++c) yreg[c] = (lab && c < a.C) ? yval(Y, col0, a.C, c) : 0.f;
     }
-    // rank sort by column (columns are unique within a row)
-    for (int e = lane; e < L; e += kWave) {
-        const int c = scol[e];
-        int rank = 0;
-        for (int u = 0; u < L; ++u) rank += scol[u] < c ? 1 : 0;
-        ocol[rank] = c;
-        od2[rank] = sd2[e];
-        if constexpr (LDS && PRE) t_idx[rank] = e;
+    // rank sort by column (columns are unique within a row).  LDS rows are read four columns
+    // per 16-B broadcast load, past L padded with INT_MAX (never below a column): a quarter of
+    // the LDS reads (a stress hub row of ~230 entries spent 5-9 us here)
+    if constexpr (LDS) {
+        const int L16 = (L + 15) & ~15;   // <= kStage, a multiple of 16
+        if (L + lane < L16) scol[L + lane] = 0x7fffffff;
+        __builtin_amdgcn_wave_barrier();   // a wave's LDS ops run in order
+        asm volatile("" ::: "memory");
+        for (int e = lane; e < L; e += kWave) {
+            const int c = scol[e];
+            int rank = 0;
+            for (int u = 0; u < L16; u += 16) {   // four loads in flight per step
+                int4 v[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const int4*>(scol + u + 4 * q);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    rank += (v[q].x < c ? 1 : 0) + (v[q].y < c ? 1 : 0) + (v[q].z < c ? 1 : 0) +
+                            (v[q].w < c ? 1 : 0);
+            }
+            ocol[rank] = c;
+            od2[rank] = sd2[e];
+            if constexpr (PRE) t_idx[rank] = e;
+        }
+    } else {
+        for (int e = lane; e < L; e += kWave) {
+            const int c = scol[e];
+            int rank = 0;
+            for (int u = 0; u < L; ++u) rank += scol[u] < c ? 1 : 0;
+            ocol[rank] = c;
+            od2[rank] = sd2[e];
+        }
     }
     if constexpr (!LDS) __threadfence();
+    GLL_ROW_PT(3);
     // sorted pass: weights, degree, labeled-prefix length
     float dsum = 0.f;
     int nlab = 0;
@@ -232,6 +297,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
     if constexpr (!LDS) __threadfence();
     dsum = wave_sum_dpp(dsum);
     nlab = wave_sum_i(nlab);
+    GLL_ROW_PT(4);
     // rhs_i = sum_{j < base} W_ij Y_j over the sorted labeled prefix, lanes over classes
     float racc[kMaxCPerLane];
 #pragma unroll
@@ -265,6 +331,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
             reinterpret_cast<float*>(sl + kVS * 2)[q % kVS] = live ? we : 0.f;
         }
     }
+    GLL_ROW_PT(5);
     if (ypre) {
         // prefetched labels: staged entry e's row of Y at ybuf[e][.], summed in sorted order
         if (lane < L && lane < kWave) {
@@ -273,13 +340,28 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
         }
         __builtin_amdgcn_wave_barrier();   // a wave's LDS ops run in order
         asm volatile("" ::: "memory");
-        for (int e0 = 0; e0 < nlab; ++e0) {
-            const int e = t_idx[e0];
-            const float we = ow[e0];
-            const float yv = lane < a.C ? (e < kWave ? ybuf[e * kYPre + lane]
-                                                     : yval(Y, ocol[e0], a.C, lane))
-                                        : 0.f;
-            racc[0] += we * yv;
+        if (L <= kWave) {   // every staged entry's labels were prefetched
+            for (int e0 = 0; e0 < nlab; ++e0) {
+                const int e = t_idx[e0];
+                racc[0] += ow[e0] * (lane < a.C ? ybuf[e * kYPre + lane] : 0.f);
+            }
+        } else {
+            // rows of hub nodes (more than 64 staged entries): 32 labeled neighbours per step,
+            // all of a step's label loads in flight before any is used (one at a time they
+            // were 15 of a stress hub row's 43 us, profiles/r05t_trace_stress.txt); the same
+            // values in the same order as the prefetched form
+            constexpr int NB = 32;
+            for (int e0 = 0; e0 < nlab; e0 += NB) {
+                float yv[NB];
+#pragma unroll
+                for (int t = 0; t < NB; ++t) {
+                    const int es = e0 + t < nlab ? e0 + t : e0;
+                    yv[t] = yval(Y, ocol[es], a.C, lane < a.C ? lane : 0);
+                }
+#pragma unroll
+                for (int t = 0; t < NB; ++t)
+                    if (e0 + t < nlab) racc[0] += ow[e0 + t] * (lane < a.C ? yv[t] : 0.f);
+            }
         }
     } else if (i >= a.base) {
         // 8 labeled neighbours per step, their label loads all in flight before any is used
@@ -314,6 +396,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
             }
         }
     }
+    GLL_ROW_PT(6);
     if (lane == 0) {
         a.row_start[i] = start;
         a.row_len[i] = L;
@@ -334,7 +417,7 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
     const int2 gxy = batch_xy<R>();   // once (per pointer it re-reads gridDim and divides)
     a.to_graph<FLAT>(gxy.y);
     Y = gshift_at(Y, ys, gxy.y);
-    __shared__ int s_col[4][kStage];
+    __shared__ __attribute__((aligned(16))) int s_col[4][kStage];
     __shared__ float s_d2[4][kStage];
     __shared__ int t_col[4][kStage];
     __shared__ float t_d2[4][kStage];
@@ -345,6 +428,9 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
     const int wv = threadIdx.x >> 6;
     const int i = gxy.x * 4 + wv;
     if (i >= a.n) return;
+#ifdef GLL_TRACE
+    const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
+#endif
     if (i == 0 && lane == 0) {   // the backward's hand-off counters start at zero
         a.fsync[0] = 0u;
         a.fsync[32] = 0u;
@@ -380,6 +466,12 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
         prd = a.rev_d2[size_t(i) * a.RCAP + lane];
     }
     const int lbound = nf + rc;
+    int tslot = -1;
+#ifdef GLL_TRACE
+    if (gxy.y == 0) tslot = i == a.base ? 0 : (rc > a.RCAP ? 10 : -1);
+    if (tslot >= 0 && lane == 0) g_trace[tslot] = t_entry;
+    GLL_ROW_PT(1);
+#endif
     int start = i * a.Wcap;
     if (lbound > a.Wcap) {
         int s0 = 0;
@@ -389,11 +481,19 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
     if (lbound <= kStage)
         build_row<true, PRE, TY, FH>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, ei, pri, prd,
                                      s_col[wv], s_d2[wv], t_col[wv], t_d2[wv], t_w[wv], t_idx[wv],
-                                     ybuf[wv]);
+                                     ybuf[wv], tslot);
     else
         build_row<false, PRE, TY, FH>(a, Y, i, start, fi, fd, fval, fmask, nf, rc, ei, pri, prd,
                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                      nullptr);
+                                      nullptr, tslot);
+#ifdef GLL_TRACE
+    if (lane_id() == 0 && gxy.y == 0) {
+        const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_entry;
+        if ((i & 15) == 0) atomicMax(&g_trace[20], dt);
+        if (rc > a.RCAP) atomicMax(&g_trace[21], dt);
+        if (tslot >= 0) g_trace[tslot + 7] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const void* Y,

@@ -260,6 +260,34 @@ def test_hub_row_longer_than_lds_chunk():
     assert np.diff(rp).max() > 256
 
 
+def test_hub_row_overflow_within_lds_staging():
+    """An unlabeled hub whose reverse list passes its capacity (8(K-1)+8 = 48 at k = 6,
+    gll_internal.h Layout::RCAP) while the row still fits the 256-entry LDS staging: its extra
+    reverse entries come from the global overflow list (rows.hip build_row, batched scan), it
+    stages more than 64 entries (the rhs loads labels past the prefetched 64, 32 per step) and
+    more than 32 of them are labeled."""
+    rng = np.random.default_rng(3)
+    n, d, base, k = 700, 64, 100, 6
+    X = rng.standard_normal((n, d))
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    hub = 300
+    v = X[hub].copy()
+    members = np.r_[10:100, 301:341]   # 90 labeled and 40 unlabeled rows around the hub
+    X[members] = v + 0.15 * rng.standard_normal((len(members), d)) / np.sqrt(d)
+    X = X.astype(np.float32)
+    lab = np.arange(n) % 10
+    Y = np.eye(10, dtype=np.float32)[lab[:base]]
+    gb = rng.standard_normal((n - base, 10))
+    U, grad = _run(X, Y, 0.07, 1.0, k, gb)
+    ind = _gpu_knn(X, k, 1.0)["knn_idx"].cpu().numpy()
+    rc = int((ind[:, 1:] == hub).sum())
+    assert 8 * (k - 1) + 8 < rc <= 250, rc
+    assert O.knn_set_mismatch(X, ind, k) == []
+    Uo, st = O.forward(X, Y, 0.07, 1.0, k, knn=(ind, None))
+    assert O.rel_err(U, Uo) < TOL
+    assert O.rel_err(grad, O.backward(st, gb)) < TOL
+
+
 @pytest.mark.parametrize("k", [10, 30])
 def test_duplicate_points_and_ties(k):
     """Clusters of exact duplicates: more tied candidates than the re-rank margin (the threshold

@@ -99,6 +99,19 @@ def timeline(tr, label):
         print("select wave 0: " + ", ".join(f"{nm} +{TICK_US * (g[q] - g[20]):.2f}" for q, nm in
                                            [(23, "row loaded"), (16, "scanned"), (17, "merged"), (18, "refined"),
                                             (19, "ranked+written")] if g[q]))
+    rw = tr[1].astype(np.int64)
+    rl = ["lists loaded", "staged (rev+ovf)", "sorted", "weights+deg", "ell/vr written", "rhs", "end"]
+    for o, nm in ((0, "row_build row base"), (10, "row_build hub row")):
+        if rw[o]:
+            print(f"{nm}: " + ", ".join(f"{rl[q - 1]} +{TICK_US * (rw[o + q] - rw[o]):.2f}"
+                                          for q in range(1, 8) if rw[o + q]) +
+                  "".join(f", {lb} +{TICK_US * (rw[o + q] - rw[o]):.2f}"
+                          for q, lb in ((8, "[overflow count read]"), (9, "[reverse list staged]")) if rw[o + q]))
+    if rw[22]:
+        print(f"row_build hub row: overflow list {rw[22]} entries, first batch matched "
+              f"+{TICK_US * (rw[23] - rw[10]):.2f}")
+    if rw[20] or rw[21]:
+        print(f"row_build longest wave: every 16th row {TICK_US * rw[20]:.2f} us, hub rows {TICK_US * rw[21]:.2f} us")
     cyc = tr[2][10:16].astype(np.int64)
     if cyc[0] and cyc[5]:
         lab = ["update+store", "publish barrier", "spmv+dots", "reduce (dpp+lds+barrier)", "alpha/beta+p,s"]
