@@ -70,11 +70,12 @@ def parse():
                     help="diagnostic: every rank on cuda:0 over gloo (RCCL refuses two ranks on "
                          "one GPU), to run the real multi-rank GPU leg on a one-GPU box; the "
                          "JSON line is marked and is no scaling measurement")
-    ap.add_argument("--autograd-thread", default="caller", choices=["caller", "device"],
+    ap.add_argument("--autograd-thread", default="auto", choices=["auto", "caller", "device"],
                     help="where torch's autograd engine runs the backward: 'caller' = the calling "
                          "thread (torch.autograd.set_multithreading_enabled(False)), 'device' = "
-                         "the engine's per-device worker thread (torch's default); the other mode "
-                         "is measured too and reported as `autograd_other_thread`")
+                         "the engine's per-device worker thread (torch's default), 'auto' = "
+                         "whichever ran a short untimed probe of each faster on this host; the "
+                         "other mode is measured too and reported as `autograd_other_thread`")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU stand-in step over gloo instead of the GPU path (launcher and "
                          "gather test; the JSON line is marked dry_run and is no measurement)")
@@ -533,6 +534,23 @@ def main():
     # engine hand-off to its device thread costs more than the step's GPU work -- ~40 us per
     # call on some boxes, profiles/r04a_host_breakdown.txt -- the calling thread keeps the
     # step GPU-bound; the other mode is timed after the run and reported beside it)
+    probe = None
+    if a.autograd_thread == "auto":
+        # untimed: a short run of each mode, the faster one is timed below (both reported)
+        probe = {}
+        for mode in ("caller", "device"):
+            with torch.autograd.set_multithreading_enabled(mode == "device"):
+                for _ in range(min(a.warmup, 5)):
+                    step()
+                gatherer.wait()
+                torch.cuda.synchronize()
+                t0_ = time.perf_counter()
+                for _ in range(min(a.steps, 100)):
+                    step()
+                gatherer.wait()
+                torch.cuda.synchronize()
+                probe[mode] = round(1e3 * (time.perf_counter() - t0_) / min(a.steps, 100), 4)
+        a.autograd_thread = min(probe, key=probe.get)
     mt = torch.autograd.set_multithreading_enabled(a.autograd_thread == "device")
     mt.__enter__()
     for _ in range(min(a.warmup, 5)):   # untimed: the first steps in this mode
@@ -743,6 +761,7 @@ def main():
             "autograd_thread": (a.autograd_thread + (" (torch.autograd.set_multithreading_enabled("
                                 f"{a.autograd_thread == 'device'}))")),
             "autograd_other_thread": other,
+            "autograd_probe_ms_per_step": probe,
             "batched": batched,
             "auto_eps_extra": auto_extra,
             "gll_env": gll_env,
