@@ -151,6 +151,28 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
             if ((t >> 6) == h) p = fbase[h] + __popcll(fmask[h] & ((1ull << (t & 63)) - 1ull));
         return p;
     };
+    // the staged position of the forward entry equal to column ri, or -1.  LDS rows scan the
+    // staged forward list [0, nf) with 16-B broadcast reads (no cross-lane chain); global-
+    // staged rows compare against the lanes' list registers
+    auto fmatch_pos = [&](int ri) {
+        if constexpr (LDS) {
+            int p = -1;
+            const int nf4 = nf & ~3;
+#pragma unroll 2
+            for (int u = 0; u < nf4; u += 4) {
+                const int4 v = *reinterpret_cast<const int4*>(scol + u);
+                p = v.x == ri ? u : p;
+                p = v.y == ri ? u + 1 : p;
+                p = v.z == ri ? u + 2 : p;
+                p = v.w == ri ? u + 3 : p;
+            }
+#pragma unroll 1
+            for (int u = nf4; u < nf; ++u) p = scol[u] == ri ? u : p;
+            return p;
+        } else {
+            return -1;   // not used
+        }
+    };
     auto fmatch = [&](int ri) {   // the forward entry equal to column ri, or -1
         int tpos = -1;
 #pragma unroll
@@ -168,7 +190,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
         const bool live = r < nr;
         const int ri = !live ? -1 : (r0 == 0 ? pri : a.rev_idx[size_t(i) * a.RCAP + r]);
         const float rd = !live ? 0.f : (r0 == 0 ? prd : a.rev_d2[size_t(i) * a.RCAP + r]);
-        const int tpos = fmatch(ri);
+        const int tpos = LDS ? fmatch_pos(ri) : fmatch(ri);
         const bool keep = live && tpos < 0;
         const uint64_t mk = __ballot(keep);
         if (keep) {
@@ -178,7 +200,8 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
         }
         if (live && tpos >= 0) {   // mutual pair: union-max (non-negative float bits order)
             if constexpr (!LDS) __threadfence();
-            atomicMax(reinterpret_cast<unsigned*>(sd2) + fpos(tpos), __float_as_uint(rd));
+            atomicMax(reinterpret_cast<unsigned*>(sd2) + (LDS ? tpos : fpos(tpos)),
+                      __float_as_uint(rd));
         }
         L += __popcll(mk);
     }
@@ -212,7 +235,7 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
                 const int oj = ojs[b], oi = ois[b];
                 const float od = ods[b];
                 const bool mine_e = oj == i;   // dead slots hold -1
-                const int tpos = __ballot(mine_e) ? fmatch(oi) : -1;
+                const int tpos = __ballot(mine_e) ? (LDS ? fmatch_pos(oi) : fmatch(oi)) : -1;
                 const bool keep = mine_e && tpos < 0;
                 const uint64_t mk = __ballot(keep);
                 if (keep) {
@@ -222,7 +245,8 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
                 }
                 if (mine_e && tpos >= 0) {   // mutual pair: union-max
                     if constexpr (!LDS) __threadfence();
-                    atomicMax(reinterpret_cast<unsigned*>(sd2) + fpos(tpos), __float_as_uint(od));
+                    atomicMax(reinterpret_cast<unsigned*>(sd2) + (LDS ? tpos : fpos(tpos)),
+                              __float_as_uint(od));
                 }
                 L += __popcll(mk);
             }
@@ -341,9 +365,22 @@ __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict
         __builtin_amdgcn_wave_barrier();   // a wave's LDS ops run in order
         asm volatile("" ::: "memory");
         if (L <= kWave) {   // every staged entry's labels were prefetched
-            for (int e0 = 0; e0 < nlab; ++e0) {
-                const int e = t_idx[e0];
-                racc[0] += ow[e0] * (lane < a.C ? ybuf[e * kYPre + lane] : 0.f);
+            // 16 entries per step: their staged indices, then their labels and weights, all
+            // read before the first product (one entry at a time was two dependent LDS round
+            // trips per labeled neighbour); same summation order
+            for (int e0 = 0; e0 < nlab; e0 += 16) {
+                int ev[16];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) ev[t] = t_idx[e0 + t < nlab ? e0 + t : e0];
+                float yv[16], wv[16];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    yv[t] = lane < a.C ? ybuf[ev[t] * kYPre + lane] : 0.f;
+                    wv[t] = ow[e0 + t < nlab ? e0 + t : e0];
+                }
+#pragma unroll
+                for (int t = 0; t < 16; ++t)
+                    if (e0 + t < nlab) racc[0] += wv[t] * yv[t];
             }
         } else {
             // rows of hub nodes (more than 64 staged entries): 32 labeled neighbours per step,
