@@ -1218,6 +1218,34 @@ def test_fused_backward_equals_two_launches_bitwise(cfg):
     assert O.rel_err(gf[0], O.backward(st, g)) <= TOL
 
 
+@pytest.mark.parametrize("live", [(3,), (0, 9), (4, 5, 6)])
+def test_fused_backward_handoff_with_uneven_column_solves(live):
+    """The fused backward's hand-off with column solves of very different
+    lengths: dL/dU is zero in all but the `live` columns, so those columns' adjoint solves run
+    their iterations while the zero columns finish at once and raise the counter first; the 125
+    gradient workgroups (one per CU, every XCD) poll while a single column is still iterating.
+    Bitwise equal to the two-launch backward, on three backwards over one workspace (re-arm), and
+    to the float64 oracle at 1e-4."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth
+    c = CONFIGS["ns"]
+    X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=21)
+    Y = one_hot(lab[: c["base"]])
+    g = np.zeros((c["batch"], 10))
+    full = seeded_gbar(c["batch"], 10, 23)
+    for q, col in enumerate(live):
+        g[:, col] = full[:, col] * 10.0 ** (3 * q)   # scales 1, 1e3, 1e6
+    Uf, gf, stf = _fwd_bwds_c_abi(X, Y, c["k"], 0.07, 1.0, g, backward_calls=3)
+    Uu, gu, stu = _fwd_bwds_c_abi(X, Y, c["k"], 0.07, 1.0, g, flags=_lib.FLAG_BWD_UNFUSED)
+    for gx in gf:
+        np.testing.assert_array_equal(gx, gu[0])
+    assert stf[_lib.ST_SOLVE_FAILED] == 0 and stf[_lib.ST_BWD_NONCONV] == 0
+    assert stf[_lib.ST_BWD_ITERS] == stu[_lib.ST_BWD_ITERS] > 0
+    ind = _gpu_knn(X, c["k"], 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, st = O.forward(X, Y, tau=0.07, epsilon=1.0, K=c["k"], knn=(ind, None))
+    assert O.rel_err(gf[0], O.backward(st, g)) <= TOL
+
+
 @pytest.mark.parametrize("cfg,B,n_extra,d", [("ns", 3, 0, None), ("fullysup", 2, 0, None),
                                              ("ns", 2, 37, 100), ("ns", 26, 0, None),
                                              ("ns", 26, 37, 100)])
