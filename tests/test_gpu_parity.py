@@ -338,6 +338,29 @@ def test_status_sink_raises_reference_warning():
     assert torch.isfinite(U).all()
 
 
+def test_negative_epsilon_is_its_absolute_value():
+    """GLL.py:233-234 use a fixed epsilon only as eps_i * eps_j, so eps < 0 gives the weights of
+    |eps| (plus the reference's 'very close to zero' style warning here): the native apply maps it
+    to |eps| with a warning, U and grad_X bitwise those of |eps| and within 1e-4 of the oracle."""
+    c = Case("ns_eps1p0_tau0p07_f32")
+    GLL = _gll()
+    gb = np.random.default_rng(4).standard_normal(c.U.shape)
+    outs = []
+    for e in (-1.0, 1.0):
+        X = torch.from_numpy(c.X).cuda().requires_grad_(True)
+        if e < 0:
+            with pytest.warns(UserWarning):
+                U = GLL.LaplaceLearningSparseHard.apply(X, torch.from_numpy(c.Y).cuda(), 0.07, e,
+                                                        c.k)
+        else:
+            U = GLL.LaplaceLearningSparseHard.apply(X, torch.from_numpy(c.Y).cuda(), 0.07, e, c.k)
+        U.backward(torch.from_numpy(gb).cuda())
+        outs.append((U.detach().cpu().numpy(), X.grad.cpu().numpy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    assert O.rel_err(outs[0][0], c.U) <= TOL
+
+
 def test_knn_sym_dist_mirror_matches_oracle():
     GLL = _gll()
     c = Case("ns_epsauto_tau0p07_f32")
