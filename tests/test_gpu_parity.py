@@ -213,6 +213,28 @@ def test_tiny_graphs(n, base, k, eps):
     assert O.rel_err(grad, O.backward(st, g)) < TOL
 
 
+@pytest.mark.parametrize("n,base,d,C,k", [(40, 39, 16, 10, 10), (60, 20, 1, 10, 10),
+                                          (60, 20, 3, 10, 10), (60, 20, 16, 1, 10),
+                                          (300, 100, 2, 1, 7)])
+@pytest.mark.parametrize("eps", [1.0, "auto"])
+def test_odd_shapes(n, base, d, C, k, eps):
+    """Shapes at the edge of the ABI: one unlabeled row, one or three features (ties in the
+    distances), a single class (label_matrix of shape [base, 1], GLL.py:32) -- U and grad_X
+    against the oracle on the GPU's own kNN lists."""
+    rng = np.random.default_rng(n + d + C)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    lab = rng.integers(0, C, base)
+    Y = np.eye(C, dtype=np.float32)[lab]
+    g = rng.standard_normal((n - base, C))
+    U, grad = _run(X, Y, 0.07, eps, k, g)
+    ind = _gpu_knn(X, k, eps)["knn_idx"].cpu().numpy().astype(np.int64)
+    assert O.knn_set_mismatch(X, ind, k) == []
+    Uo, st = O.forward(X, Y, 0.07, eps, k, knn=(ind, None))
+    assert U.shape == (n - base, C)
+    assert O.rel_err(U, Uo) < TOL
+    assert O.rel_err(grad, O.backward(st, g)) < TOL
+
+
 @pytest.mark.parametrize("n,base,k", [(8, 2, 10), (12, 3, 10), (66, 1, 57)])
 def test_batched_tiny_graphs(n, base, k):
     """The batched entry on three graphs of a handful of points (k clipped to n; k = 57 on 66
