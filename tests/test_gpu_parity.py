@@ -235,6 +235,26 @@ def test_odd_shapes(n, base, d, C, k, eps):
     assert O.rel_err(grad, O.backward(st, g)) < TOL
 
 
+@pytest.mark.parametrize("d", [1028, 2048, 4096])
+def test_wide_features_up_to_the_limit(d):
+    """Features past the fused backward's 1,024 and up to include/gll.h's 4,096: the Gram's
+    feature phases, the exact re-rank over d-float rows and the feature gradient past the
+    register-row form, against the oracle."""
+    rng = np.random.default_rng(d)
+    n, base, k = 300, 100, 10
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    lab = rng.integers(0, 10, base)
+    Y = np.eye(10, dtype=np.float32)[lab]
+    g = rng.standard_normal((n - base, 10))
+    U, grad = _run(X, Y, 0.07, 1.0, k, g)
+    ind = _gpu_knn(X, k, 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    assert O.knn_set_mismatch(X, ind, k) == []
+    Uo, st = O.forward(X, Y, 0.07, 1.0, k, knn=(ind, None))
+    assert O.rel_err(U, Uo) < TOL
+    assert O.rel_err(grad, O.backward(st, g)) < TOL
+
+
 @pytest.mark.parametrize("n,base,k", [(8, 2, 10), (12, 3, 10), (66, 1, 57)])
 def test_batched_tiny_graphs(n, base, k):
     """The batched entry on three graphs of a handful of points (k clipped to n; k = 57 on 66
