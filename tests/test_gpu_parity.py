@@ -255,6 +255,27 @@ def test_wide_features_up_to_the_limit(d):
     assert O.rel_err(grad, O.backward(st, g)) < TOL
 
 
+@pytest.mark.parametrize("eps", [1.0, "auto"])
+def test_batch_of_one_equals_the_single_graph(eps):
+    """X of shape [1, n, d] through the batched entry against X [n, d] through the single-graph
+    one: the same predictions and feature gradient (1e-5: the batched launch may run another CG
+    geometry), U of shape [1, m, C]."""
+    from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth
+    GLL = _gll()
+    c = CONFIGS["ns"]
+    X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=31)
+    Y = one_hot(lab[: c["base"]])
+    g = seeded_gbar(c["batch"], 10, 37)
+    U1, g1 = _run(X, Y, 0.07, eps, c["k"], g)
+    Xb = torch.from_numpy(X[None]).cuda().requires_grad_(True)
+    Ub = GLL.LaplaceLearningSparseHard.apply(Xb, torch.from_numpy(Y[None]).cuda(), 0.07, eps,
+                                             c["k"])
+    assert tuple(Ub.shape) == (1,) + U1.shape
+    Ub.backward(torch.from_numpy(g[None]).cuda())
+    assert O.rel_err(Ub[0].detach().cpu().numpy(), U1) <= 1e-5
+    assert O.rel_err(Xb.grad[0].cpu().numpy(), g1) <= 1e-5
+
+
 @pytest.mark.parametrize("n,base,k", [(8, 2, 10), (12, 3, 10), (66, 1, 57)])
 def test_batched_tiny_graphs(n, base, k):
     """The batched entry on three graphs of a handful of points (k clipped to n; k = 57 on 66
