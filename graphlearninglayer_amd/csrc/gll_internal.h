@@ -205,7 +205,8 @@ struct Layout {
     int dp;           // split-Gram planes: d rounded up to 64
     size_t xhi, xlo, xnrm;   // [n][dp] bf16 hi / lo planes of x - x_0, and |x - x_0|^2
     size_t fsync;     // fused backward: [0] solved columns, [32] finished gradient blocks,
-                      // [64] poison (a lost solve: the counters may be stale)
+                      // [64] poison (a lost solve: the counters may be stale), [96] release
+                      // (set by the last column to arrive; the gradient blocks poll it)
     size_t d2s;       // float: the fp16 D2 scale of the pre-split GEMM (knn.hip tile_d2_scale)
     size_t pid, perm; // locality order (order_rows): nearest pivot of each row, the row order
     size_t ohist;     // locality order: rows per pivot of each 64-row block ([ceil(n/64)][64])
@@ -262,7 +263,7 @@ struct Layout {
         xhi = take(size_t(n) * dp * 2);
         xlo = take(size_t(n) * dp * 2);
         xnrm = take(size_t(n) * 4);
-        fsync = take(384);   // three words on their own 128-B lines, zeroed by row_build
+        fsync = take(512);   // four words on their own 128-B lines, zeroed by row_build
         d2s = take(256);     // fp16 D2 scale of the pre-split Gram (knn.hip tile_d2_scale)
         pid = take(size_t(n) * 4);
         perm = take(size_t(n) * 4);

@@ -472,6 +472,7 @@ __global__ __launch_bounds__(256) void row_build_kernel(RowArgs a, const TY* __r
         a.fsync[0] = 0u;
         a.fsync[32] = 0u;
         a.fsync[64] = 0u;   // a poisoned workspace (lost solve) is rebuilt here
+        a.fsync[96] = 0u;
     }
     if (i == 0 && a.gsync)   // single graphs only (grid_cg_route)
         for (int t = lane; t < kGridSyncWords; t += kWave) a.gsync[t] = 0u;

@@ -527,8 +527,12 @@ __device__ __forceinline__ void cg_ell_body(
     if (fsync) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0)
-            __hip_atomic_fetch_add(fsync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the column completing the count writes the release word the gradient blocks poll
+        // (on its own line: the pollers never read the line the arrivals add to)
+        if (tid == 0 &&
+            __hip_atomic_fetch_add(fsync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u ==
+                unsigned(C))
+            __hip_atomic_store(fsync + 96, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     GLL_TRACE_PT(9);
 }
@@ -1095,11 +1099,12 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
         int ok = __hip_atomic_load(fsync + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
         unsigned spins = 0;
         const unsigned long long t0 = wall_ticks();
-        // ~n_poll x 256 cycles between polls: 125 workgroups polling the line the solves add
-        // to would otherwise queue those adds behind a storm of loads
-        while (ok && __hip_atomic_load(fsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-               unsigned(C)) {
-            for (int q = 0; q < 4; ++q) __builtin_amdgcn_s_sleep(4);
+        // the release word (fsync[96]) sits on a line no arrival adds to, so the 125 pollers
+        // may poll it closely (round 4 polled the counter line itself with ~1,000 cycles
+        // between polls, so as not to queue the columns' adds behind the loads)
+        while (ok && __hip_atomic_load(fsync + 96, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               0u) {
+            __builtin_amdgcn_s_sleep(2);
             if ((++spins & 15u) == 0 && wall_ticks() - t0 > kWaitTicks) {   // 1 s of wall clock
                 ok = 0;
                 break;
@@ -1177,6 +1182,7 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
             __hip_atomic_load(fsync + 64, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
             __hip_atomic_store(fsync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(fsync + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(fsync + 96, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
