@@ -1171,15 +1171,21 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
         // workspace (retain_graph) -- unless some workgroup gave up on the solves: then CG
         // workgroups may still add to fsync[0] after a reset, so the workspace is poisoned
         // instead (fsync[64], cleared by the next forward's row build)
+        // Relaxed agent-scope atomics throughout (all performed at the coherence point, §3.5):
+        // an acquire-release count made every one of the 125 gradient workgroups write back and
+        // invalidate its XCD's L2 (buffer_wbl2 / buffer_inv) on its way out.  The poison is
+        // performed before this workgroup's count (the vmcnt wait on the returning atomic), so
+        // the last workgroup, whose count follows every other, reads it.
         if (!ok) {
             __hip_atomic_fetch_or(fsync + 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (st_failed) atomicOr(st_failed, 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         const unsigned ng = gridDim.x - unsigned(C);
-        const unsigned old = __hip_atomic_fetch_add(fsync + 32, 1u, __ATOMIC_ACQ_REL,
+        const unsigned old = __hip_atomic_fetch_add(fsync + 32, 1u, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
         if (old + 1u == ng &&
-            __hip_atomic_load(fsync + 64, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+            __hip_atomic_load(fsync + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
             __hip_atomic_store(fsync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(fsync + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(fsync + 96, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
