@@ -21,7 +21,7 @@ from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth  #
 
 EPS = {"plumbing": 1.0, "ns": 1.0, "fullysup": 1.0, "stress": "auto"}
 ap = argparse.ArgumentParser()
-ap.add_argument("--flags", default="0,4")
+ap.add_argument("--flags", default="0")
 ap.add_argument("--configs", default="ns")
 ap.add_argument("--batch", default="1,64")
 ap.add_argument("--reps", type=int, default=50)
