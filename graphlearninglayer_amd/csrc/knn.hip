@@ -1276,10 +1276,14 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // ranks in float64 -- used where fp32 cannot separate two candidates.  Either
 // way the (i, j) and (j, i) sums run the same lane mapping on negated differences: bitwise
 // symmetric for the same ACC.  Lanes outside [lo, hi) keep `ce`.
-template <bool VEC, int PG, typename ACC, int NU = 16, bool XL = false>
-__device__ __forceinline__ ACC exact_d2(const float* __restrict__ X, const float* __restrict__ xi,
-                                        int i, int d, int ci, int lo, int hi, ACC ce,
-                                        const float* xs = nullptr) {
+// FULL: d is a multiple of 32 NU, so every feature step is in range -- no clamped addresses and
+// no masks (the masked form adds exact zeros there: the same sums bit for bit).  Single-graph
+// selects: NS 12.4 -> 11.7-12.1 us, FullySup 22.0 -> 21.3-21.5 us, stress unchanged
+// (profiles/r05zx_ab_select_unmasked_gated.txt).
+template <bool VEC, int PG, typename ACC, int NU, bool XL, bool FULL>
+__device__ __forceinline__ ACC exact_d2_body(const float* __restrict__ X,
+                                             const float* __restrict__ xi, int i, int d, int ci,
+                                             int lo, int hi, ACC ce, const float* xs) {
     constexpr bool F64 = std::is_same<ACC, double>::value;
     const int lane = lane_id();
     const int grp = lane >> 3, sub = lane & 7;
@@ -1300,9 +1304,16 @@ __device__ __forceinline__ ACC exact_d2(const float* __restrict__ X, const float
 #pragma unroll
             for (int u = 0; u < NU; ++u) {   // straight-line: every load issued before use
                 const int k = kb + 32 * u + 4 * sub;
-                if constexpr (!XL) va[u] = load4_raw<VEC>(xi, k, d);
+                if constexpr (FULL) {
+                    if constexpr (!XL) va[u] = *reinterpret_cast<const f32x4*>(xi + k);
 #pragma unroll
-                for (int g2 = 0; g2 < PG; ++g2) vb[g2][u] = load4_raw<VEC>(xj[g2], k, d);
+                    for (int g2 = 0; g2 < PG; ++g2)
+                        vb[g2][u] = *reinterpret_cast<const f32x4*>(xj[g2] + k);
+                } else {
+                    if constexpr (!XL) va[u] = load4_raw<VEC>(xi, k, d);
+#pragma unroll
+                    for (int g2 = 0; g2 < PG; ++g2) vb[g2][u] = load4_raw<VEC>(xj[g2], k, d);
+                }
 
             }
 #pragma unroll
@@ -1313,7 +1324,8 @@ __device__ __forceinline__ ACC exact_d2(const float* __restrict__ X, const float
                     if constexpr (XL)   // x_i from the wave's LDS copy, read at use
                         va[u] = *reinterpret_cast<const f32x4*>(xs + k);
                     if constexpr (F64) {
-                        const f32x4 a = mask4<VEC>(va[u], k, d), b = mask4<VEC>(vb[g2][u], k, d);
+                        const f32x4 a = FULL ? va[u] : mask4<VEC>(va[u], k, d);
+                        const f32x4 b = FULL ? vb[g2][u] : mask4<VEC>(vb[g2][u], k, d);
                         const double d0 = double(a.x) - double(b.x), d1 = double(a.y) - double(b.y);
                         const double d2 = double(a.z) - double(b.z), d3 = double(a.w) - double(b.w);
                         part[g2] = __builtin_fma(d0, d0, part[g2]);
@@ -1324,7 +1336,7 @@ __device__ __forceinline__ ACC exact_d2(const float* __restrict__ X, const float
                         // explicit fma chain: contraction left to the compiler differed
                         // between instantiations (packed multiplies, then adds), and with it
                         // the last bit of d^2 between the select's two forms
-                        const f32x4 df = mask4<VEC>(va[u] - vb[g2][u], k, d);
+                        const f32x4 df = FULL ? va[u] - vb[g2][u] : mask4<VEC>(va[u] - vb[g2][u], k, d);
                         part[g2] = __builtin_fmaf(df.x, df.x, part[g2]);
                         part[g2] = __builtin_fmaf(df.y, df.y, part[g2]);
                         part[g2] = __builtin_fmaf(df.z, df.z, part[g2]);
@@ -1348,6 +1360,19 @@ __device__ __forceinline__ ACC exact_d2(const float* __restrict__ X, const float
         }
     }
     return ce;
+}
+
+template <bool VEC, int PG, typename ACC, int NU = 16, bool XL = false>
+__device__ __forceinline__ ACC exact_d2(const float* __restrict__ X, const float* __restrict__ xi,
+                                        int i, int d, int ci, int lo, int hi, ACC ce,
+                                        const float* xs = nullptr) {
+    // only the single-graph sweep (NU = 16): in the occupancy forms (x_i in LDS, <= 64 / 80
+    // VGPRs, NU = 4) a second body -- theirs or the rescan's / refinement's -- spilled (B = 64 NS
+    // select 159 -> 186 us, profiles/r05zw_ab_select_unmasked.txt)
+    if constexpr (VEC && !XL && NU >= 16)
+        if (d % (32 * NU) == 0)
+            return exact_d2_body<VEC, PG, ACC, NU, XL, true>(X, xi, i, d, ci, lo, hi, ce, xs);
+    return exact_d2_body<VEC, PG, ACC, NU, XL, false>(X, xi, i, d, ci, lo, hi, ce, xs);
 }
 
 // Rank of this lane's (exact d^2, index) key among lanes [0, cnt); lanes without a candidate
