@@ -1280,7 +1280,7 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // no masks (the masked form adds exact zeros there: the same sums bit for bit).  Single-graph
 // selects: NS 12.4 -> 11.7-12.1 us, FullySup 22.0 -> 21.3-21.5 us, stress unchanged
 // (profiles/r05zx_ab_select_unmasked_gated.txt).
-template <bool VEC, int PG, typename ACC, int NU, bool XL, bool FULL>
+template <bool VEC, int PG, typename ACC, int NU, bool XL, bool FULL, bool SPLIT = false>
 __device__ __forceinline__ ACC exact_d2_body(const float* __restrict__ X,
                                              const float* __restrict__ xi, int i, int d, int ci,
                                              int lo, int hi, ACC ce, const float* xs) {
@@ -1299,12 +1299,14 @@ __device__ __forceinline__ ACC exact_d2_body(const float* __restrict__ X,
         ACC part[PG];
 #pragma unroll
         for (int g2 = 0; g2 < PG; ++g2) part[g2] = ACC(0);
-        for (int kb = 0; kb < d; kb += 32 * NU) {   // NU steps of 32 features: loads in flight
+        // one step of NU x 32 features, every load in flight; F: no masks (in range)
+        auto step = [&](const int kb, auto full) {
+            constexpr bool F = decltype(full)::value;
             f32x4 va[NU], vb[PG][NU];
 #pragma unroll
             for (int u = 0; u < NU; ++u) {   // straight-line: every load issued before use
                 const int k = kb + 32 * u + 4 * sub;
-                if constexpr (FULL) {
+                if constexpr (F) {
                     if constexpr (!XL) va[u] = *reinterpret_cast<const f32x4*>(xi + k);
 #pragma unroll
                     for (int g2 = 0; g2 < PG; ++g2)
@@ -1324,8 +1326,8 @@ __device__ __forceinline__ ACC exact_d2_body(const float* __restrict__ X,
                     if constexpr (XL)   // x_i from the wave's LDS copy, read at use
                         va[u] = *reinterpret_cast<const f32x4*>(xs + k);
                     if constexpr (F64) {
-                        const f32x4 a = FULL ? va[u] : mask4<VEC>(va[u], k, d);
-                        const f32x4 b = FULL ? vb[g2][u] : mask4<VEC>(vb[g2][u], k, d);
+                        const f32x4 a = F ? va[u] : mask4<VEC>(va[u], k, d);
+                        const f32x4 b = F ? vb[g2][u] : mask4<VEC>(vb[g2][u], k, d);
                         const double d0 = double(a.x) - double(b.x), d1 = double(a.y) - double(b.y);
                         const double d2 = double(a.z) - double(b.z), d3 = double(a.w) - double(b.w);
                         part[g2] = __builtin_fma(d0, d0, part[g2]);
@@ -1336,7 +1338,7 @@ __device__ __forceinline__ ACC exact_d2_body(const float* __restrict__ X,
                         // explicit fma chain: contraction left to the compiler differed
                         // between instantiations (packed multiplies, then adds), and with it
                         // the last bit of d^2 between the select's two forms
-                        const f32x4 df = FULL ? va[u] - vb[g2][u] : mask4<VEC>(va[u] - vb[g2][u], k, d);
+                        const f32x4 df = F ? va[u] - vb[g2][u] : mask4<VEC>(va[u] - vb[g2][u], k, d);
                         part[g2] = __builtin_fmaf(df.x, df.x, part[g2]);
                         part[g2] = __builtin_fmaf(df.y, df.y, part[g2]);
                         part[g2] = __builtin_fmaf(df.z, df.z, part[g2]);
@@ -1344,6 +1346,17 @@ __device__ __forceinline__ ACC exact_d2_body(const float* __restrict__ X,
                     }
                 }
             }
+        };
+        if constexpr (FULL) {
+            for (int kb = 0; kb < d; kb += 32 * NU) step(kb, std::true_type{});
+        } else if constexpr (SPLIT) {
+            // the whole steps unmasked, then at most one masked step
+            const int df = d - d % (32 * NU);
+            int kb = 0;
+            for (; kb < df; kb += 32 * NU) step(kb, std::true_type{});
+            if (kb < d) step(kb, std::false_type{});
+        } else {
+            for (int kb = 0; kb < d; kb += 32 * NU) step(kb, std::false_type{});
         }
 #pragma unroll
         for (int g2 = 0; g2 < PG; ++g2) {
@@ -1368,11 +1381,13 @@ __device__ __forceinline__ ACC exact_d2(const float* __restrict__ X, const float
                                         const float* xs = nullptr) {
     // only the single-graph sweep (NU = 16): in the occupancy forms (x_i in LDS, <= 64 / 80
     // VGPRs, NU = 4) a second body -- theirs or the rescan's / refinement's -- spilled (B = 64 NS
-    // select 159 -> 186 us, profiles/r05zw_ab_select_unmasked.txt)
+    // select 159 -> 186 us, profiles/r05zw_ab_select_unmasked.txt).  Those take SPLIT instead:
+    // one body, whole steps unmasked and at most one masked step (B = 64 NS select 161 -> 148 us,
+    // FullySup 332 -> 315 us, profiles/r05zy_ab_select_split_b64.txt)
     if constexpr (VEC && !XL && NU >= 16)
         if (d % (32 * NU) == 0)
             return exact_d2_body<VEC, PG, ACC, NU, XL, true>(X, xi, i, d, ci, lo, hi, ce, xs);
-    return exact_d2_body<VEC, PG, ACC, NU, XL, false>(X, xi, i, d, ci, lo, hi, ce, xs);
+    return exact_d2_body<VEC, PG, ACC, NU, XL, false, VEC && XL>(X, xi, i, d, ci, lo, hi, ce, xs);
 }
 
 // Rank of this lane's (exact d^2, index) key among lanes [0, cnt); lanes without a candidate
