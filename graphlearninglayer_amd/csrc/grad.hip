@@ -92,9 +92,11 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
     const int beg = a.row_start[i], end = beg + a.row_len[i];
     const float ei = a.eps_fixed > 0.f ? a.eps_fixed : a.eps[i];
     const float* xi = X + size_t(i) * d;
-    f32x4 xv[ND];   // x_i, loaded up front: its latency hides behind the edge loop
+    // x_i, loaded up front: its latency hides behind the edge loop.  Rows are read unmasked
+    // (load4_raw: lanes past d read in-bounds clamped addresses, and their sums are never stored)
+    f32x4 xv[ND];
 #pragma unroll
-    for (int q = 0; q < ND; ++q) xv[q] = load4<VEC>(xi, 4 * lane + 4 * kWave * q, d);
+    for (int q = 0; q < ND; ++q) xv[q] = load4_raw<VEC>(xi, 4 * lane + 4 * kWave * q, d);
     int kth_i = 0;
     float b_i = 0.f;
     if constexpr (AUTO) {
@@ -141,7 +143,7 @@ __global__ __launch_bounds__(256) void grad_spmm_kernel(EdgeArgs a, const float*
                 s[u] = t0 + u < cnt ? readlane_f(cf, t) : 0.f;
                 const float* xj = X + size_t(readlane_i(cj, t)) * d;
 #pragma unroll
-                for (int q = 0; q < ND; ++q) v[u][q] = load4<VEC>(xj, 4 * lane + 4 * kWave * q, d);
+                for (int q = 0; q < ND; ++q) v[u][q] = load4_raw<VEC>(xj, 4 * lane + 4 * kWave * q, d);
             }
 #pragma unroll
             for (int u = 0; u < EB; ++u) {

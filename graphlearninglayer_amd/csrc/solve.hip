@@ -1040,7 +1040,7 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
     const float* xi = X + size_t(i) * d;
     f32x4 xv[ND];
 #pragma unroll
-    for (int q = 0; q < ND; ++q) xv[q] = load4<true>(xi, 4 * lane + 4 * kWave * q, d);
+    for (int q = 0; q < ND; ++q) xv[q] = load4_raw<true>(xi, 4 * lane + 4 * kWave * q, d);
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     float pi[NC];
 #pragma unroll
@@ -1090,7 +1090,7 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
         const int t = u < cnt0 ? u : 0;
         const float* xj = X + size_t(readlane_i(cj, t)) * d;
 #pragma unroll
-        for (int q = 0; q < ND; ++q) v[u][q] = load4<true>(xj, 4 * lane + 4 * kWave * q, d);
+        for (int q = 0; q < ND; ++q) v[u][q] = load4_raw<true>(xj, 4 * lane + 4 * kWave * q, d);
     }
     // ---- wait for the C column solves (bounded: a lost solve surfaces as NaN + status)
     if (threadIdx.x == 0) {
@@ -1136,7 +1136,7 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
                     const int t = t0 + u < cnt ? t0 + u : t0;
                     const float* xj = X + size_t(readlane_i(cj, t)) * d;
 #pragma unroll
-                    for (int q = 0; q < ND; ++q) v[u][q] = load4<true>(xj, 4 * lane + 4 * kWave * q, d);
+                    for (int q = 0; q < ND; ++q) v[u][q] = load4_raw<true>(xj, 4 * lane + 4 * kWave * q, d);
                 }
             }
 #pragma unroll
