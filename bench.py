@@ -36,7 +36,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from graphlearninglayer_amd import GLL, _lib  # noqa: E402
-from graphlearninglayer_amd.parallel import PredictionGatherer, shard_rank_seed  # noqa: E402
+from graphlearninglayer_amd.parallel import (PredictionGatherer, distinct_devices,  # noqa: E402
+                                              rank_identity, shard_rank_seed)
 from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth  # noqa: E402
 
 METRIC = "GLL fwd+bwd calls/sec (base=500,batch=500,d=512,k=10) at 1/2/4/8 GPU"
@@ -173,25 +174,59 @@ def cg_roofline_extras(work_spmv, work_iter, avg_s, traffic):
     return out
 
 
-# C-ABI kernel ids (gll_kernel_name) -> device symbols as rocprofv3 names them
-PMC_SYMBOLS = {"gram_d2_kernel": ["gram_pk_kernel", "gram_bf3s_kernel", "gram_bf3_kernel", "gram_bf3w_kernel", "gram48_kernel",
-                                   "gram_lds_kernel", "gram_wide_kernel"], "knn_select_kernel": ["knn_select_kernel"],
+# C-ABI kernel ids (gll_kernel_name) -> device symbols as rocprofv3 names them.  The Gram id
+# covers several launches on the pre-split route: gram_split_kernel (hi/lo planes),
+# gram_pk2_kernel (the main 256-tile GEMM) and gram_pk_kernel (its 128-subtile tail); single
+# small graphs run gram_bf3s_kernel alone.  The main kernel is listed first.
+PMC_SYMBOLS = {"gram_d2_kernel": ["gram_pk2_kernel", "gram_bf3s_kernel", "gram_bf3w_kernel",
+                                  "gram_bf3_kernel", "gram_pk_kernel"],
+               "knn_select_kernel": ["knn_select_kernel", "knn_select_wide_kernel"],
                "row_build_kernel": ["row_build_kernel"],
-               "cg_kernel": ["cg_ell_kernel", "cg_vr_kernel", "cg_grid_kernel", "cg_lds_kernel"],
+               "cg_kernel": ["cg_ell_kernel", "cg_vr_kernel", "cg_gv_kernel", "cg_grid_kernel",
+                             "cg_lds_kernel"],
                "edge_coef_kernel": ["edge_coef_kernel"], "grad_spmm_kernel": ["grad_spmm_kernel", "grad_chunk_kernel"],
                "cg_grad_fused_kernel": ["cg_grad_fused_kernel"]}
+# the Gram's launches by role, for the MFMA counters (reported separately)
+GRAM_ROLES = (("main", "gram_pk2_kernel"), ("tail", "gram_pk_kernel"),
+              ("single", "gram_bf3s_kernel"), ("inline", "gram_bf3w_kernel"),
+              ("inline", "gram_bf3_kernel"))
+
+
+def build_profile_tags():
+    """Profile-session tags recorded against THIS library build (profiles/<tag>_build.json,
+    written by tools/prof_session.sh with the library's gll_build_id), newest first.  bench.py
+    cites only these: a summary of another build is never cited, whatever its name."""
+    import glob
+    bid = _lib.build_id()
+    tags = []
+    for p in glob.glob(os.path.join(ROOT, "profiles", "*_build.json")):
+        try:
+            with open(p) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if doc.get("build_id") == bid:
+            tags.append((doc.get("recorded", ""), os.path.basename(p)[: -len("_build.json")]))
+    return [t for _, t in sorted(tags, reverse=True)]
+
+
+def _build_profile(name_of_tag):
+    """profiles/<file> of the newest session of this build holding it, or None."""
+    for tag in build_profile_tags():
+        rel = os.path.join("profiles", name_of_tag(tag))
+        if os.path.exists(os.path.join(ROOT, rel)):
+            return rel
+    return None
 
 
 def pmc_traffic(config, kernel):
-    """HBM-side bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/rNN_pmc_<config>.json, written by tools/pmc_summary.py from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command), or None."""
-    import glob
-    here = os.path.dirname(os.path.abspath(__file__))
-    paths = sorted(glob.glob(os.path.join(here, "profiles", f"r*_pmc_{config}.json")))
-    if not paths:
+    """HBM-side bytes per launch of `kernel` from this build's PMC summary
+    (profiles/<tag>_pmc_<config>.json, tools/pmc_summary.py over separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this same bench command), or None."""
+    rel = _build_profile(lambda t: f"{t}_pmc_{config}.json")
+    if rel is None:
         return None
-    with open(paths[-1]) as f:
+    with open(os.path.join(ROOT, rel)) as f:
         doc = json.load(f)
     for sym in PMC_SYMBOLS.get(kernel, []):
         if sym in doc["kernels"]:
@@ -199,34 +234,49 @@ def pmc_traffic(config, kernel):
     return None
 
 
-def _newest_profile(pattern):
-    """The newest committed summary matching `pattern` (profiles/<tag>_<cfg>_..., tags sort by
-    round: tools/prof_session.sh + tools/collect_profiles.sh write them)."""
-    import glob
-    here = os.path.dirname(os.path.abspath(__file__))
-    paths = sorted(glob.glob(os.path.join(here, "profiles", pattern)))
-    return os.path.join("profiles", os.path.basename(paths[-1])) if paths else None
+def rocprof_stats(config):
+    """This build's rocprofv3 --kernel-trace --stats summary of `config`, or None."""
+    return _build_profile(lambda t: f"{t}_{config}_kernel_stats.csv")
+
+
+def rocprof_avg_us(rel, kernel):
+    """Mean rocprof duration (us) over every launch of the symbols of C-ABI kernel `kernel`
+    in a committed kernel_stats CSV."""
+    import csv
+    if rel is None:
+        return None
+    tot_ns, calls = 0.0, 0
+    with open(os.path.join(ROOT, rel)) as f:
+        for row in csv.DictReader(f):
+            name = row["Name"]
+            if any(f"::{sym}<" in name or f"::{sym}(" in name for sym in PMC_SYMBOLS[kernel]):
+                tot_ns += float(row["TotalDurationNs"])
+                calls += int(row["Calls"])
+    return round(tot_ns / calls / 1e3, 3) if calls else None
 
 
 def gram_mfma_pmc(config):
-    """The Gram's MFMA counters from the newest committed summary (profiles/rNN_mfma_<config>.json,
+    """The Gram's MFMA counters from this build's summary (profiles/<tag>_mfma_<config>.json,
     tools/mfma_summary.py over a rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16
-    SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE pass), or None."""
-    import glob
-    here = os.path.dirname(os.path.abspath(__file__))
-    paths = sorted(glob.glob(os.path.join(here, "profiles", f"r*_mfma_{config}.json")))
-    if not paths:
+    SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE pass), each Gram launch by role
+    (main GEMM, tail, single-graph kernel), or None."""
+    rel = _build_profile(lambda t: f"{t}_mfma_{config}.json")
+    if rel is None:
         return None
-    with open(paths[-1]) as f:
+    with open(os.path.join(ROOT, rel)) as f:
         doc = json.load(f)
-    for sym in PMC_SYMBOLS["gram_d2_kernel"]:
+    out = {}
+    for role, sym in GRAM_ROLES:
         e = doc["kernels"].get(sym)
-        if e and "exec_bf16_tflops" in e:
-            return {"kernel": sym, "exec_bf16_tflops": e["exec_bf16_tflops"],
-                    "exec_frac_of_bf16_peak": e["exec_flops_frac_of_peak"],
-                    "mfma_busy_frac": e.get("mfma_busy_frac"), "duration_us": e["duration_us"],
-                    "source": os.path.join("profiles", os.path.basename(paths[-1]))}
-    return None
+        if e and "exec_bf16_tflops" in e and role not in out:
+            out[role] = {"kernel": sym, "exec_bf16_tflops": e["exec_bf16_tflops"],
+                         "exec_frac_of_bf16_peak": e["exec_flops_frac_of_peak"],
+                         "mfma_busy_frac": e.get("mfma_busy_frac"),
+                         "duration_us": e["duration_us"]}
+    if not out:
+        return None
+    out["source"] = rel
+    return out
 
 
 def batched_measure(c, eps, tau, k, B, gstats, dev, rank, steps=20, warmup=5):
@@ -287,7 +337,13 @@ def batched_measure(c, eps, tau, k, B, gstats, dev, rank, steps=20, warmup=5):
             "frac": round(achieved / HBM_PEAK_GBS, 5), "spmv_frac": round(achieved / HBM_PEAK_GBS, 5),
             "work_per_launch": B * work, "avg_launch_us": round(avg_s * 1e6, 3),
             "launches": cnt, "traffic": traffic,
-            "rocprof_stats": _newest_profile(f"*_{c['name']}_b{B}_kernel_stats.csv")}
+            "rocprof_stats": rocprof_stats(f"{c['name']}_b{B}")}
+    # the same SpMV roofline from this build's committed rocprofv3 summary (the profiler's
+    # kernel durations read ~2 us longer than the dispatch-packet events per launch)
+    rp_us = rocprof_avg_us(roof["rocprof_stats"], "cg_kernel")
+    roof["rocprof_avg_launch_us"] = rp_us
+    roof["spmv_frac_rocprof"] = (round(B * work / (rp_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)
+                                 if rp_us else None)
     roof.update(cg_roofline_extras(B * work, B * cg_iter_work, avg_s, traffic))
     return {"B": B, "value": round(B * steps / elapsed, 3), "unit": "calls/s",
             "ms_per_step": round(1e3 * elapsed / steps, 4),
@@ -441,11 +497,13 @@ def dry_run(a, world, rank):
             for r in range(world):
                 ok &= bool(torch.equal(full[s, r], base_u + r + 1000.0 * (a.warmup + s)))
         ok &= full.shape[0] == a.steps
+    ident = rank_identity(None, torch.device("cpu"))   # outside the timed region
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "dry_run": True, "unit": "calls/s",
                           "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                           "ms_per_step": round(1e3 * elapsed / max(a.steps, 1), 4),
                           "gather_check": "ok" if ok else "FAILED",
+                          "ranks": ident, "distinct_gpus": distinct_devices(ident),
                           "config": {"workload": "dry-run stand-in", "parallelism": f"dp{world}"}}),
               flush=True)
     if world > 1:
@@ -573,6 +631,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # which GPU each rank ran on, as the process group sees it (one tiny all_gather, outside the
+    # timed region): a scaling line carries its own proof of N distinct devices and N ranks
+    ident = rank_identity(dev, coll)
+    distinct = distinct_devices(ident)
+    if world > 1 and not distinct and not a.share_gpu and rank == 0:
+        print(f"bench.py: ranks did not report {world} distinct GPUs: {ident}", file=sys.stderr)
+
     gather_check = None
     if world > 1:
         # every rank's inputs are fixed, so each slot of the last gathered group must hold
@@ -615,7 +680,11 @@ def main():
                     "avg_launch_us": round(avg_s * 1e6, 3), "launches": cnt,
                     "cg_iters_fwd_bwd": list(iters),
                     "gram_mfma_pmc": gram_mfma_pmc(a.config),
-                    "rocprof_stats": _newest_profile(f"*_{a.config}_kernel_stats.csv")}
+                    "rocprof_stats": rocprof_stats(a.config)}
+        rp_us = rocprof_avg_us(roofline["rocprof_stats"], dominant)
+        roofline["rocprof_avg_launch_us"] = rp_us
+        roofline["frac_rocprof"] = (round((work / (rp_us * 1e-6) / (1e12 if bound == "mfma" else 1e9))
+                                          / peak, 5) if rp_us else None)
         if dominant == "cg_kernel":
             roofline["definition"] = ("SURVEY §8d SpMV roofline: B_spmv x iterations / CG launch "
                                       "time / 8 TB/s, B_spmv = 8 nnz_off(Luu) + 8 m + 8 m C")
@@ -749,6 +818,9 @@ def main():
             "config": {"workload": a.config, "base": c["base"], "batch": c["batch"], "d": c["d"],
                        "k": k, "eps": eps, "tau": tau, "classes": 10,
                        "parallelism": f"dp{world}", "upstream_grad": "fixed seeded dL/dU",
+                       # the autograd engine's threading mode the value was timed in (part of the
+                       # workload's identity: compare lines across rounds only at equal modes)
+                       "autograd_thread": a.autograd_thread,
                        "collective": (("gloo all_gather(U) staged through the host, one per "
                                        f"{GATHER_EVERY} calls" if a.share_gpu else
                                        f"async all_gather(U) over RCCL, one per {GATHER_EVERY} calls")
@@ -756,6 +828,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "gather_check": gather_check,
+            "ranks": ident,
+            "distinct_gpus": distinct,
             "kernels": per_kernel,
             "c_abi": c_abi,
             "autograd_thread": (a.autograd_thread + (" (torch.autograd.set_multithreading_enabled("
@@ -765,6 +839,8 @@ def main():
             "batched": batched,
             "auto_eps_extra": auto_extra,
             "gll_env": gll_env,
+            "build_id": _lib.build_id(),
+            "profiles_of_this_build": build_profile_tags(),
         }
         if foreign:
             out["invalid"] = (f"GLL_* variables that change what runs are set ({', '.join(foreign)}): "

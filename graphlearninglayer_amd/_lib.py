@@ -44,7 +44,7 @@ EXPORTS = (
     "gll_workspace_bytes", "gll_forward", "gll_backward", "gll_forward_batched",
     "gll_backward_batched", "gll_graph", "gll_workspace_view",
     "gll_cg_csr_workspace_bytes", "gll_cg_csr", "gll_prof_enable", "gll_prof_read",
-    "gll_kernel_name", "gll_strerror", "gll_set_knob",
+    "gll_kernel_name", "gll_strerror", "gll_set_knob", "gll_build_id",
 )
 
 
@@ -97,7 +97,14 @@ def _declare(lib):
     lib.gll_set_knob.restype = i32
     lib.gll_strerror.argtypes = [i32]
     lib.gll_strerror.restype = ct.c_char_p
+    lib.gll_build_id.argtypes = []
+    lib.gll_build_id.restype = ct.c_char_p
     return lib
+
+
+def build_id() -> str:
+    """The loaded library's build identity (build.py source_digest at its build)."""
+    return lib().gll_build_id().decode()
 
 
 def lib():

@@ -43,7 +43,15 @@ def _headers_mtime():
 def _compile(unit, force, verbose, extra, objdir=OBJ):
     src = os.path.join(CSRC, unit)
     obj = os.path.join(objdir, unit.replace(".hip", ".o"))
-    if (not force and os.path.exists(obj)
+    stamp = obj + ".id"
+    if unit == "api.hip":
+        # api.hip carries the build identity (gll_build_id): rebuilt whenever any input changed
+        bid = source_digest()
+        extra = [*extra, f'-DGLL_BUILD_ID="{bid}"']
+        fresh_id = os.path.exists(stamp) and open(stamp).read() == bid
+    else:
+        fresh_id = True
+    if (not force and fresh_id and os.path.exists(obj)
             and os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime())):
         return obj
     cmd = [hipcc(), *FLAGS, *extra, "-c", src, "-o", obj]
@@ -64,7 +72,25 @@ def _compile(unit, force, verbose, extra, objdir=OBJ):
         raise RuntimeError(f"{unit} kept changing while it compiled")
     if verbose and r.stderr.strip():
         print(r.stderr, file=sys.stderr)
+    if unit == "api.hip":
+        with open(stamp, "w") as fh:
+            fh.write(bid)
     return obj
+
+
+def source_digest() -> str:
+    """Build identity of libgll.so: sha256 (16 hex) over every source and header it is built
+    from and the compile flags.  Profile sessions record it (profiles/<tag>_build.json) and
+    bench.py cites only the summaries whose identity equals the library it measures."""
+    import hashlib
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    hs = sorted(f for f in os.listdir(CSRC) if f.endswith(".h"))
+    for f in [*UNITS, *hs]:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    with open(os.path.join(INCLUDE, "gll.h"), "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def _inputs_digest(src):
@@ -156,7 +182,11 @@ def main():
                     help="print per-kernel VGPR/SGPR/LDS/occupancy (-Rpass-analysis)")
     ap.add_argument("--trace", action="store_true",
                     help="also build the in-kernel timestamp variant _obj/libgll_trace.so")
+    ap.add_argument("--digest", action="store_true", help="print the build identity and exit")
     a = ap.parse_args()
+    if a.digest:
+        print(source_digest())
+        return
     if a.trace:
         print(build_trace(force=a.force, verbose=a.verbose))
     extra = ["-Rpass-analysis=kernel-resource-usage"] if a.resource_usage else []

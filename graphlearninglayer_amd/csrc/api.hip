@@ -407,6 +407,11 @@ const char* gll_kernel_name(int kid) {
     return kKernelNames[kid];
 }
 
+#ifndef GLL_BUILD_ID
+#define GLL_BUILD_ID "unknown"
+#endif
+const char* gll_build_id(void) { return GLL_BUILD_ID; }
+
 const char* gll_strerror(int code) {
     switch (code) {
         case GLL_OK: return "ok";

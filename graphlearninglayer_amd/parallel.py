@@ -115,3 +115,56 @@ class PredictionGatherer:
         self.inflight = []
         if self.keep is not None and len(self.gathered) > self.keep:
             del self.gathered[: len(self.gathered) - self.keep]
+
+
+def _pci_fields(dev) -> tuple:
+    """(domain, bus, device, uuid hash) of a GPU, all -1 for a CPU rank."""
+    if dev is None or dev.type != "cuda":
+        return (-1, -1, -1, -1)
+    import hashlib
+    p = torch.cuda.get_device_properties(dev)
+    uu = int.from_bytes(hashlib.sha256(str(getattr(p, "uuid", "")).encode()).digest()[:7], "little")
+    return (int(getattr(p, "pci_domain_id", -1)), int(getattr(p, "pci_bus_id", -1)),
+            int(getattr(p, "pci_device_id", -1)), uu)
+
+
+def rank_identity(dev=None, coll=None, group=None) -> list:
+    """Every rank's (rank, LOCAL_RANK, current device, PCI address, world size it sees), as the
+    process group itself gathers them: one tiny all_gather, called outside any timed region.
+
+    This makes a scaling run self-proving (each of N ranks on its own GPU, RCCL seeing N
+    ranks).  `dev` is the rank's GPU (None: a CPU rank), `coll` the device the collective
+    moves tensors on (the GPU for RCCL, the CPU for gloo).  Without a process group it
+    returns this process alone."""
+    import os
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cur = torch.cuda.current_device() if dev is not None and dev.type == "cuda" else -1
+    if dist.is_available() and dist.is_initialized():
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+    else:
+        rank, world = 0, 1
+    mine = torch.tensor([rank, local, cur, *_pci_fields(dev), world], dtype=torch.int64)
+    if world > 1 or (dist.is_available() and dist.is_initialized()):
+        mine = mine.to(coll if coll is not None else "cpu")
+        allr = torch.empty(world * mine.numel(), dtype=torch.int64, device=mine.device)
+        dist.all_gather_into_tensor(allr, mine, group=group)
+        rows = allr.view(world, -1).cpu().tolist()
+    else:
+        rows = [mine.tolist()]
+    out = []
+    for r, lr, cd, dom, bus, pdev, uu, ws in rows:
+        out.append({"rank": r, "local_rank": lr, "current_device": cd,
+                    "pci": (f"{dom:04x}:{bus:02x}:{pdev:02x}" if bus >= 0 else None),
+                    "uuid_hash": (f"{uu:014x}" if uu >= 0 else None),
+                    "world_size_seen": ws})
+    return out
+
+
+def distinct_devices(ident: list) -> bool:
+    """True when no two ranks report the same GPU (PCI address and device UUID) and every rank
+    saw as many ranks as there are entries."""
+    gpus = [(e["pci"], e["uuid_hash"]) for e in ident if e["pci"] is not None]
+    sizes = {e["world_size_seen"] for e in ident}
+    ranks = sorted(e["rank"] for e in ident)
+    return (len(set(gpus)) == len(gpus) and sizes == {len(ident)}
+            and ranks == list(range(len(ident))))

@@ -179,8 +179,9 @@ int gll_workspace_view(const gll_problem* p, void* workspace, gll_view* out);
  * max_iter.  `iters` (device int, may be NULL) receives the max iteration count,
  * `nonconv` (device int, may be NULL) the columns that hit max_iter.  `workspace`
  * (gll_cg_csr_workspace_bytes) holds the Krylov vectors: required when m > 2048 (those
- * systems run as one cooperative launch over the whole GPU, C <= 16), may be NULL when
- * 5 m floats fit in LDS. */
+ * systems run on the whole GPU as one ordinary launch sized within the co-resident
+ * workgroup capacity, C <= 16; a lost grid barrier is rescued by one workgroup solving
+ * alone, counted in GLL_ST_GRID_RESCUED), may be NULL when 5 m floats fit in LDS. */
 size_t gll_cg_csr_workspace_bytes(int m, int C);
 int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const float* val,
                const float* b, float* x, float atol, int max_iter, int32_t* iters,
@@ -190,7 +191,8 @@ int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const f
  * bracketed by HIP events on its stream (p = 0 disables); gll_prof_read synchronises those
  * events and returns the summed milliseconds and the number of bracketed launches, then
  * clears them. */
-#define GLL_K_GRAM 0      /* gram_d2_kernel: fp32 MFMA squared distances */
+#define GLL_K_GRAM 0      /* gram_d2_kernel: squared distances on split-bf16 MFMA (x = hi + lo,
+                           * three bf16 products; candidates only, the select re-ranks exactly) */
 #define GLL_K_SELECT 1    /* knn_select_kernel: top-K + exact re-rank + reverse scatter */
 #define GLL_K_FINALIZE 2  /* row_build_kernel: symmetric rows, W, degree, rhs */
 #define GLL_K_CG 3        /* cg_*_kernel: Jacobi-CG solves (forward and adjoint) */
@@ -202,6 +204,11 @@ int gll_cg_csr(int m, int C, const int32_t* row_ptr, const int32_t* col, const f
 int gll_prof_enable(int kid, int period);
 int gll_prof_read(int kid, double* ms_total, int* count);
 const char* gll_kernel_name(int kid);
+
+/* Build identity: sha256 (16 hex) of the sources, headers and flags this library was built
+ * from (graphlearninglayer_amd/build.py source_digest).  bench.py cites only profiles
+ * recorded against the same identity. */
+const char* gll_build_id(void);
 
 /* Human-readable message for a return code. */
 const char* gll_strerror(int code);

@@ -33,7 +33,7 @@ from oracle import graphlearning_standin  # noqa: E402
 
 REF = "/root/reference/GLL.py"
 
-# (config, epsilon, tau, label dtype)
+# (config, epsilon, tau, label dtype[, overrides of C / k])
 CASES = [
     ("plumbing", 1.0, 0.07, "f32"),
     ("plumbing", 1.0, 0.0, "f32"),
@@ -46,6 +46,16 @@ CASES = [
     ("fullysup", 1.0, 0.07, "f32"),
     ("adv", "auto", 0.0, "i64"),
     ("stress", "auto", 0.07, "f32"),    # BASELINE config 5 (projected grad, ~11 s here)
+    # Round 6: the reference pins the paths the HIP build takes only for C != 10 or wide k
+    # (it takes any label_matrix.shape[1], GLL.py:32,85, and any k through the spy, GLL.py:27)
+    ("ns", 1.0, 0.07, "f32", dict(C=3)),
+    ("ns", "auto", 0.07, "f32", dict(C=3)),
+    ("ns", 1.0, 0.07, "f32", dict(C=17)),
+    ("ns", "auto", 0.0, "i64", dict(C=17)),
+    ("ns", 1.0, 0.07, "f32", dict(k=64)),
+    ("ns", "auto", 0.07, "f32", dict(k=100)),
+    # eps = 0: W = exp(-4 d^2 / 0) = 0 and V = -8 W / 0 = NaN (GLL.py:233-234): U = 0, grad NaN
+    ("plumbing", 0.0, 0.07, "f32"),
 ]
 EXTRA = {"adv": dict(base=100, batch=1000, d=200, k=25, r=1.0)}
 FULL_GRAD_MAX_N = 256
@@ -71,15 +81,18 @@ def sample_rows(n, seed=PROJ_SEED):
     return np.sort(rng.choice(n, size=min(N_ROWS, n), replace=False))
 
 
-def case_name(cfg, eps, tau, ydt):
-    return f"{cfg}_eps{eps}_tau{tau}_{ydt}".replace(".", "p")
+def case_name(cfg, eps, tau, ydt, ov=None):
+    sfx = "".join(f"_{key}{val}" for key, val in sorted((ov or {}).items()))
+    return f"{cfg}_eps{eps}_tau{tau}_{ydt}{sfx}".replace(".", "p")
 
 
-def run_case(mod, cfg, eps, tau, ydt):
+def run_case(mod, cfg, eps, tau, ydt, ov=None):
     p = dict(CONFIGS.get(cfg) or EXTRA[cfg])
+    p.update(ov or {})
     base, batch, d, k, r = p["base"], p["batch"], p["d"], p["k"], p["r"]
-    X, labels = synth(base, batch, d, C=10, r=r, seed=0)
-    Yf = one_hot(labels[:base], 10)
+    C = p.get("C", 10)
+    X, labels = synth(base, batch, d, C=C, r=r, seed=0)
+    Yf = one_hot(labels[:base], C)
     Y = torch.from_numpy(Yf) if ydt == "f32" else torch.from_numpy(Yf).long()
     orig = mod.knn_sym_dist
     captured = {}
@@ -93,14 +106,14 @@ def run_case(mod, cfg, eps, tau, ydt):
     try:
         Xt = torch.from_numpy(X).requires_grad_(True)
         U = mod.LaplaceLearningSparseHard.apply(Xt, Y, tau, eps)
-        gbar = seeded_gbar(batch, 10)
+        gbar = seeded_gbar(batch, C)
         U.backward(torch.from_numpy(gbar))
         grad = Xt.grad.detach().numpy().astype(np.float64)
     finally:
         mod.knn_sym_dist = orig
     out = dict(
         meta=json.dumps(dict(cfg=cfg, base=base, batch=batch, d=d, k=k, r=r, seed=0,
-                             eps=eps, tau=tau, ydtype=ydt, C=10, x_sha256=sha256(X),
+                             eps=eps, tau=tau, ydtype=ydt, C=C, x_sha256=sha256(X),
                              gbar_seed=1234, proj_seed=PROJ_SEED)),
         U=U.detach().numpy(),
         knn=np.asarray(captured["knn"]).astype(np.int16 if base + batch < 32768 else np.int32),
@@ -123,13 +136,15 @@ def run_case(mod, cfg, eps, tau, ydt):
 # restated step by step below with utils.py line numbers.
 LAPLACE = dict(labeled=250, unlabeled=2750, d=64, knn_num=50, epsilon=1.0, tau=1e-8, r=1.0,
                seed=21)
+# fixture file -> overrides of LAPLACE (round 6: knn_num = 64 takes the wide kNN select)
+LAPLACE_CASES = {"laplace_small": {}, "laplace_k64": dict(knn_num=64, unlabeled=1250)}
 
 
-def run_laplace(mod):
+def run_laplace(mod, ov=None):
     import scipy.sparse as sparse
     from oracle.gll_oracle import one_hot_encode
 
-    p = LAPLACE
+    p = dict(LAPLACE, **(ov or {}))
     X, labels = synth(p["labeled"], p["unlabeled"], p["d"], C=10, r=p["r"], seed=p["seed"])
     train = labels[: p["labeled"]]
     W, _, _, _, knn = mod.knn_sym_dist(X, k=p["knn_num"], epsilon=p["epsilon"])   # utils.py:574
@@ -143,7 +158,7 @@ def run_laplace(mod):
     M = sparse.spdiags(1 / np.sqrt(M + 1e-10), 0, m, m).tocsr()                    # utils.py:587
     pred = mod.stable_conjgrad(M * Luu * M, -M * Lul @ Y)                          # utils.py:589-590
     pred = M * pred                                                                # utils.py:591
-    meta = dict(LAPLACE, x_sha256=sha256(X), C=10)
+    meta = dict(p, x_sha256=sha256(X), C=10)
     return dict(meta=json.dumps(meta), U=np.asarray(pred),
                 knn=np.asarray(knn).astype(np.int16), labels=labels.astype(np.int16))
 
@@ -153,17 +168,20 @@ def main():
     only = sys.argv[1:]
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     mod = load_reference()
-    if not only or any("laplace_small".startswith(o) for o in only):
-        lap = run_laplace(mod)
-        path = os.path.join(HERE, "laplace_small.npz")
+    for lname, lov in LAPLACE_CASES.items():
+        if only and not any(lname.startswith(o) for o in only):
+            continue
+        lap = run_laplace(mod, lov)
+        path = os.path.join(HERE, lname + ".npz")
         np.savez_compressed(path, **lap)
-        print(f"laplace_small: U max {np.abs(lap['U']).max():.4g} -> "
+        print(f"{lname}: U max {np.abs(lap['U']).max():.4g} -> "
               f"{os.path.getsize(path)/1024:.0f} KB")
-    for cfg, eps, tau, ydt in CASES:
-        name = case_name(cfg, eps, tau, ydt)
+    for cfg, eps, tau, ydt, *ov in CASES:
+        ov = ov[0] if ov else None
+        name = case_name(cfg, eps, tau, ydt, ov)
         if only and not any(name.startswith(o) for o in only):
             continue
-        out = run_case(mod, cfg, eps, tau, ydt)
+        out = run_case(mod, cfg, eps, tau, ydt, ov)
         path = os.path.join(HERE, name + ".npz")
         np.savez_compressed(path, **out)
         print(f"{name}: U max {np.abs(out['U']).max():.4g} -> {os.path.getsize(path)/1024:.0f} KB")

@@ -31,7 +31,7 @@ class Case:
         self.z = z
         self.meta = json.loads(str(z["meta"]))
         m = self.meta
-        self.X, labels = synth(m["base"], m["batch"], m["d"], r=m["r"], seed=m["seed"])
+        self.X, labels = synth(m["base"], m["batch"], m["d"], C=m["C"], r=m["r"], seed=m["seed"])
         self.x_ok = sha256(self.X) == m["x_sha256"]
         if "X" in z:
             self.X = z["X"]
@@ -55,11 +55,28 @@ class Case:
         return self.meta["k"]
 
     def grad_error(self, grad, rel_err):
-        """Parity metric of a full n x d gradient against the stored reference gradient."""
+        """Parity metric of a full n x d gradient against the stored reference gradient.
+
+        NaN entries of the reference (eps = 0: V = -8 W / 0, GLL.py:234) must be NaN at the
+        same places; the metric then runs over the finite entries (0 when there are none)."""
         z = self.z
         grad = np.asarray(grad, dtype=np.float64)
         if "grad" in z:
-            return rel_err(grad, z["grad"])
-        e1 = rel_err(grad @ projection(self.meta["d"]), z["grad_proj"])
-        e2 = rel_err(grad[z["grad_rows_idx"]], z["grad_rows"])
+            return nan_aware(rel_err)(grad, z["grad"])
+        e1 = nan_aware(rel_err)(grad @ projection(self.meta["d"]), z["grad_proj"])
+        e2 = nan_aware(rel_err)(grad[z["grad_rows_idx"]], z["grad_rows"])
         return max(e1, e2)
+
+
+def nan_aware(rel_err):
+    """rel_err over finite entries, +inf when the NaN patterns of a and b differ."""
+    def f(a, b):
+        a = np.asarray(a, dtype=np.float64)
+        b = np.asarray(b, dtype=np.float64)
+        na, nb = np.isnan(a), np.isnan(b)
+        if not np.array_equal(na, nb):
+            return float("inf")
+        if nb.all():
+            return 0.0
+        return rel_err(a[~nb], b[~nb])
+    return f

@@ -63,5 +63,15 @@ def test_rccl_gather_of_predictions_at_world_one():
         work.wait()
         assert out.shape == Us[0].shape and torch.equal(out, Us[0])
         assert np.isfinite(gx.cpu().numpy()).all()
+        # bench.py's self-proving fields (rank_identity: one all_gather over RCCL)
+        from graphlearninglayer_amd.parallel import distinct_devices, rank_identity
+        ident = rank_identity(dev, dev)
+        assert len(ident) == 1 and ident[0]["rank"] == 0 and ident[0]["world_size_seen"] == 1
+        assert ident[0]["current_device"] == 0
+        p = torch.cuda.get_device_properties(dev)
+        assert ident[0]["pci"] == f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+        assert ident[0]["uuid_hash"] is not None
+        assert distinct_devices(ident)
+        print("rank identity:", ident)
     finally:
         dist.destroy_process_group()

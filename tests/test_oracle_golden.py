@@ -9,7 +9,7 @@ import torch
 
 from oracle import gll_oracle as O
 from oracle import gll_port as PT
-from tests.golden_io import Case, names
+from tests.golden_io import Case, nan_aware, names
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -17,7 +17,20 @@ CASES = names()
 
 
 def test_fixtures_present():
-    assert len(CASES) >= 10
+    assert len(CASES) >= 18
+    # round 6: the reference itself pins C != 10, wide k and eps = 0
+    for want in ("ns_eps1p0_tau0p07_f32_C3", "ns_epsauto_tau0p0_i64_C17",
+                 "ns_eps1p0_tau0p07_f32_k64", "ns_epsauto_tau0p07_f32_k100",
+                 "plumbing_eps0p0_tau0p07_f32"):
+        assert want in CASES
+
+
+def test_eps_zero_fixture_is_the_reference_nan_gradient():
+    """GLL.py:233-234 with eps = 0: W = exp(-inf) = 0 -> U = 0; V = -8 * 0 / 0 = NaN -> the
+    whole feature gradient is NaN.  The fixture records exactly that."""
+    c = Case("plumbing_eps0p0_tau0p07_f32")
+    assert np.all(c.U == 0)
+    assert np.isnan(c.z["grad"]).all()
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -30,9 +43,10 @@ def test_oracle_matches_reference(name):
     c = Case(name)
     ind, _ = O.knn_exact(c.X, c.k)
     assert np.array_equal(ind, c.knn)
-    U, st = O.forward(c.X, c.Y, c.tau, c.eps, c.k)
-    assert O.rel_err(U, c.U) < 1e-12
-    grad = O.backward(st, c.gbar)
+    with np.errstate(divide="ignore", invalid="ignore"):   # eps = 0 divides by zero
+        U, st = O.forward(c.X, c.Y, c.tau, c.eps, c.k)
+        grad = O.backward(st, c.gbar)
+    assert nan_aware(O.rel_err)(U, c.U) < 1e-12
     # the reference casts the edge values to fp32 before G @ X (GLL.py:154): fp32 floor
     assert c.grad_error(grad, O.rel_err) < 2e-6
 
@@ -41,9 +55,10 @@ def test_oracle_matches_reference(name):
 def test_port_matches_reference(name):
     c = Case(name)
     Xt = torch.from_numpy(c.X).requires_grad_(True)
-    U, saved = PT.forward(Xt, torch.from_numpy(c.Y), c.tau, c.eps, c.k)
-    assert O.rel_err(U.numpy(), c.U) < 1e-12
-    g = PT.backward(saved, torch.from_numpy(c.gbar)).numpy()
+    with np.errstate(divide="ignore", invalid="ignore"):
+        U, saved = PT.forward(Xt, torch.from_numpy(c.Y), c.tau, c.eps, c.k)
+        g = PT.backward(saved, torch.from_numpy(c.gbar)).numpy()
+    assert nan_aware(O.rel_err)(U.numpy(), c.U) < 1e-12
     assert c.grad_error(g, O.rel_err) < 2e-6
 
 
@@ -70,12 +85,13 @@ def test_fd_gradient_plumbing():
     assert abs(fd - an) / abs(an) < 1e-6
 
 
-def test_oracle_laplace_matches_reference_fixture():
+@pytest.mark.parametrize("fname", ["laplace_small", "laplace_k64"])
+def test_oracle_laplace_matches_reference_fixture(fname):
     """utils.laplace: the closed-form oracle vs the reference pipeline
     (reference knn_sym_dist + stable_conjgrad driven by utils.py:570-593's glue)."""
     import json
     from graphlearninglayer_amd.synth import sha256, synth
-    z = np.load(os.path.join(GOLDEN, "laplace_small.npz"))
+    z = np.load(os.path.join(GOLDEN, fname + ".npz"))
     p = json.loads(str(z["meta"]))
     X, labels = synth(p["labeled"], p["unlabeled"], p["d"], C=10, r=p["r"], seed=p["seed"])
     assert sha256(X) == p["x_sha256"]

@@ -159,6 +159,24 @@ def test_bench_launches_its_own_ranks_dry_run():
     assert out["n_gpus"] == 2 and out["steps"] == 17 and out["dry_run"] is True
     assert out["gather_check"] == "ok"
     assert out["config"]["parallelism"] == "dp2"
+    # the self-proving fields of a scaling line: both ranks, as the process group saw them
+    ranks = out["ranks"]
+    assert [e["rank"] for e in ranks] == [0, 1]
+    assert [e["local_rank"] for e in ranks] == [0, 1]
+    assert all(e["world_size_seen"] == 2 for e in ranks)
+    assert all(e["pci"] is None and e["current_device"] == -1 for e in ranks)   # CPU stand-in
+    assert out["distinct_gpus"] is True
+
+
+def test_distinct_devices_rejects_a_shared_gpu():
+    from graphlearninglayer_amd.parallel import distinct_devices
+    a = {"rank": 0, "local_rank": 0, "current_device": 0, "pci": "0000:05:00",
+         "uuid_hash": "01", "world_size_seen": 2}
+    b = dict(a, rank=1, local_rank=1, current_device=1, pci="0000:15:00", uuid_hash="02")
+    assert distinct_devices([a, b])
+    assert not distinct_devices([a, dict(b, pci="0000:05:00", uuid_hash="01")])
+    assert not distinct_devices([a, dict(b, world_size_seen=1)])
+    assert not distinct_devices([a, dict(b, rank=0)])
 
 
 def test_bench_rejects_world_size_mismatch():

@@ -12,6 +12,6 @@ for d in gpurun_out/${T}_prof_*; do
   f=$(find "$d" -name '*kernel_stats.csv' | head -1)
   [[ -n $f ]] && cp "$f" "profiles/${T}_${cfg}_kernel_stats.csv" && echo "profiles/${T}_${cfg}_kernel_stats.csv"
 done
-for f in gpurun_out/${T}_pmc_*.json gpurun_out/${T}_mfma_*.json; do
+for f in gpurun_out/${T}_pmc_*.json gpurun_out/${T}_mfma_*.json gpurun_out/${T}_build.json; do
   [[ -f $f ]] && cp "$f" profiles/ && echo "profiles/$(basename "$f")"
 done

@@ -29,8 +29,12 @@ for cfg in $CFGS; do
   steps+=("${T}_prof_${cfg}:180:$env_part $P $ST_ARGS -d gpurun_out/${T}_prof_${cfg} -o run -- $prog")
   steps+=("${T}_pmcf_${cfg}:150:$env_part $P --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/${T}_pmcf_${cfg} -o run -- $prog")
   steps+=("${T}_pmcw_${cfg}:150:$env_part $P --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/${T}_pmcw_${cfg} -o run -- $prog")
-  case $cfg in ns_b64|stress) steps+=("${T}_mfma_${cfg}:150:$env_part $P $MF -d gpurun_out/${T}_mfma_${cfg} -o run -- $prog");; esac
+  case $cfg in ns|ns_b64|stress) steps+=("${T}_mfma_${cfg}:150:$env_part $P $MF -d gpurun_out/${T}_mfma_${cfg} -o run -- $prog");; esac
 done
+# the build identity these summaries belong to (bench.py cites a summary only for its own build)
+python3 -c "import json, time; from graphlearninglayer_amd import _lib; \
+json.dump({'build_id': _lib.build_id(), 'recorded': time.strftime('%Y-%m-%dT%H:%M:%S'), \
+'tag': '$T'}, open('gpurun_out/${T}_build.json', 'w'))"
 bash tools/gpu_steps.sh "${steps[@]}"
 rc=$?
 for cfg in $CFGS; do
