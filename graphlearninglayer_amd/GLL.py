@@ -31,7 +31,7 @@ import torch
 from . import _lib
 
 DEFAULT_K = 25          # GLL.py:27
-MAX_K = 129             # include/gll.h: 2 <= K <= 129 (neighbours incl. self; kMaxKm1Wide = 128)
+MAX_K = 257             # include/gll.h: 2 <= K <= 257 (neighbours incl. self; kMaxKm1Huge = 256)
 DEFAULT_RTOL = 1e-6     # fp32 Jacobi-CG at 1e-6 matches SuperLU to <1e-5
 DEFAULT_MAX_ITER = 1000
 

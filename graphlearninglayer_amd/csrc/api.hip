@@ -163,7 +163,7 @@ static int check(const gll_problem* p) {
     if (p->n < 2 || p->d < 1 || p->C < 1 || p->K < 2) return GLL_ERR_INVALID_ARG;
     if (p->base < 0 || p->base > p->n) return GLL_ERR_INVALID_ARG;
     const int K = p->K < p->n ? p->K : p->n;
-    if (K - 1 > kMaxKm1Wide) return GLL_ERR_UNSUPPORTED;  // the wide select's LDS lists
+    if (K - 1 > kMaxKm1Huge) return GLL_ERR_UNSUPPORTED;  // the wide select's LDS lists
     if (p->flags & ~GLL_FLAG_ALL) return GLL_ERR_INVALID_ARG;   // unknown (or retired) flags
     if (p->C > 256) return GLL_ERR_UNSUPPORTED;       // rhs accumulators per lane
     if ((p->d + 255) / 256 > 16) return GLL_ERR_UNSUPPORTED;  // d <= 4096 in the SpMM

@@ -16,7 +16,8 @@ namespace gll {
 constexpr int kWave = 64;
 constexpr int kMaxKm1 = 56;      // K - 1 <= 56: knn_select_kernel (one candidate per lane; the
                                  // rescan keeps >= 8 lanes of a wave free)
-constexpr int kMaxKm1Wide = 128; // K - 1 <= 128: knn_select_wide_kernel (LDS lists; k <= 129)
+constexpr int kMaxKm1Wide = 128; // K - 1 <= 128: knn_select_wide_kernel, 256 candidate slots
+constexpr int kMaxKm1Huge = 256; // K - 1 <= 256: the same kernel with 512 slots (k <= 257)
 
 // ---------------------------------------------------------------------------------------
 // Workspace layout.  One block per forward/backward pair, carved into 256-B aligned arrays.
@@ -24,8 +25,8 @@ constexpr int kMaxKm1Wide = 128; // K - 1 <= 128: knn_select_wide_kernel (LDS li
 //
 // Graph storage ("padded rows"): row i of the symmetric kNN graph holds row_len[i] entries
 // (col, w, d2) starting at row_start[i], sorted by column.  Ordinary rows sit in a fixed slot
-// i * Wcap (Wcap = (K-1) + RCAP); rows whose reverse list overflowed (hubs) get their
-// storage from a bump region behind the slots.  No prefix sum over rows is ever needed.
+// i * Wcap (Wcap = 5(K-1) + 8); rows longer than that (hubs) get their storage from a bump
+// region behind the slots.  No prefix sum over rows is ever needed.
 // ---------------------------------------------------------------------------------------
 constexpr int kStOvfCount = 8;   // internal status words: overflow-list length
 constexpr int kStBump = 9;       //                        bump-region cursor
@@ -55,8 +56,10 @@ constexpr int kVrSlot = kVS * 2 + kVS * 4;   // 48 B
 // threads of the balanced kernel: 512, up to 10 virtual rows each in 256 VGPRs (1024 threads
 // hold at most 5 in 128 VGPRs and spilled: 118 against 66 us per FullySup solve)
 constexpr int kVrNT = 512;
-// (at most 63: the CG's virtual-row map keeps the slot in 6 bits; longer rows keep their tail
-// in the CSR, which the balanced kernel's spill path sums)
+// Virtual-row slots per U row: enough for a row of Layout::Wcap = 5(K-1)+8 entries (the row
+// slot); hub rows in the bump region can be longer, and so can rows at k > 101, where the
+// 6-bit slot field of the CG's virtual-row map caps this at 63: their tail stays in the CSR and
+// the balanced kernel's spill path sums it (tests force both: the VRM clamp and the spill).
 inline int vr_max_per_row(int K) {
     const int v = ((K - 1) + 4 * (K - 1) + 8 + kVS - 1) / kVS;
     return v < 63 ? v : 63;
@@ -223,7 +226,12 @@ struct Layout {
         // list, which each such (hub) row then scans whole -- at stress (K = 30) 4(K-1)+8 left
         // 39 hubs scanning 742 entries, 14 of their 35 us (profiles/r05w_trace_stress.txt)
         RCAP = 8 * (K - 1) + 8;
-        Wcap = (K - 1) + RCAP;
+        // A row's slot holds its forward list and up to 4(K-1)+8 reverse entries (~1.4(K-1)
+        // entries on average); longer rows -- hubs -- take their storage from the bump region,
+        // which holds every row at once if it must (all rows together have at most 2n(K-1)
+        // entries).  The slot width is kept apart from RCAP: the six Etot arrays cost 24 B a
+        // slot, and a 9(K-1)+8-wide slot made them 60% larger for every graph.
+        Wcap = (K - 1) + 4 * (K - 1) + 8;
         Etot = int64_t(n) * Wcap + 2LL * n * (K - 1);
         size_t off = 0;
         auto take = [&](size_t bytes) {

@@ -1720,8 +1720,8 @@ void knn_select_kernel(
 }
 
 // --------------------------------------------------------------------------------------
-// Wide kNN select (kMaxKm1 < K - 1 <= kMaxKm1Wide: k up to 129 incl. self, e.g. utils.laplace
-// with knn_num = 64 or 100, utils.py:574).  knn_select_kernel holds one candidate per lane, so
+// Wide kNN select (kMaxKm1 < K - 1 <= kMaxKm1Huge: k up to 257 incl. self, e.g. utils.laplace
+// with knn_num = 64, 100 or 200, utils.py:574).  knn_select_kernel holds one candidate per lane, so
 // its list (K - 1 plus a re-rank margin) and the rescan's lanes cap K - 1 at 56.  Here a wave
 // keeps its row's candidates in LDS (kWideCap slots) and its running K - 1 nearest as a sorted
 // list in LDS, and ranks in float64 throughout:
@@ -1737,23 +1737,21 @@ void knn_select_kernel(
 //      the bound is streamed through the same merge (GLL_ST_KNN_RESCAN).
 // Exact for any input like the narrow kernel; distances are the float64 sums rounded once.
 // --------------------------------------------------------------------------------------
-constexpr int kWideCap = 256;   // candidate slots per row
-constexpr int kWideTop = 4;     // per-lane list entries of the threshold scan (64 x 4 >= kc)
-
-struct WideLists {
-    int cj[kWideCap];          // candidates: column
-    uint32_t cg[kWideCap];     // candidates: Gram D2 bits
+// Two tiers share the kernel: K - 1 <= 128 (kMaxKm1Wide) with 256 candidate slots and per-lane
+// lists of 4, and K - 1 <= 256 (kMaxKm1Huge, round 6) with 512 slots and lists of 5 (64 x 5 >=
+// kc = K - 1 + 8); the LDS lists of a wave are 5.5 / 10.5 KiB.
+template <int CAP, int KMX>
+struct WideListsT {
+    int cj[CAP];               // candidates: column
+    uint32_t cg[CAP];          // candidates: Gram D2 bits
     double cd[kWave];          // a chunk's float64 distances
-    int bj[2][kMaxKm1Wide];    // sorted K - 1 nearest (double-buffered merge)
-    double bd[2][kMaxKm1Wide];
+    int bj[2][KMX];            // sorted K - 1 nearest (double-buffered merge)
+    double bd[2][KMX];
 };
 
-// Merge a chunk (lanes < cnt hold candidate cj) into the sorted list `cur` of nb entries:
-// float64 distances, then every entry's rank in the union by (d^2, index); the first K - 1 go
-// to the other buffer.  Returns the new length.  Deterministic (a strict total order).
-template <bool VEC>
+template <bool VEC, typename WL>
 __device__ __forceinline__ int wide_absorb(const float* __restrict__ X, const float* __restrict__ xi,
-                                           int i, int d, int Km1, int cj, int cnt, WideLists& w,
+                                           int i, int d, int Km1, int cj, int cnt, WL& w,
                                            int& cur, int nb) {
     const int lane = lane_id();
     double dv = exact_d2<VEC, 1, double, 4>(X, xi, i, d, lane < cnt ? cj : -1, 0, cnt,
@@ -1797,7 +1795,7 @@ __device__ __forceinline__ int wide_absorb(const float* __restrict__ X, const fl
     return min(nb + valid, Km1);
 }
 
-template <bool VEC, int NP>
+template <bool VEC, int NP, int CAP, int KMX, int TOP>
 __global__ __launch_bounds__(256) void knn_select_wide_kernel(
     const float* __restrict__ D2, int ld, size_t plane, const float* __restrict__ X, int n, int d,
     int K, int kc, float eps_fixed, int auto_eps, int RCAP, int32_t* __restrict__ knn_idx,
@@ -1817,7 +1815,9 @@ __global__ __launch_bounds__(256) void knn_select_wide_kernel(
     ovf = gshift_at(ovf, wss, gxy.y);
     status = gshift_at(status, wss, gxy.y);
     status_pub = gshift_at(status_pub, sts, gxy.y);
-    __shared__ WideLists s_w[4];
+    constexpr int kWideCap = CAP;
+    constexpr int kWideTop = TOP;
+    __shared__ WideListsT<CAP, KMX> s_w[4];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
     int i;
@@ -1829,7 +1829,7 @@ __global__ __launch_bounds__(256) void knn_select_wide_kernel(
         i = r0 + gxy.x * 4 + wv;
         if (i >= r1) return;    // whole wave
     }
-    WideLists& w = s_w[wv];
+    WideListsT<CAP, KMX>& w = s_w[wv];
     const int Km1 = K - 1;
     const D2Row<false> row{reinterpret_cast<const char*>(D2) + size_t(i - r0) * ld * 4, 1.f};
     auto bits_of = [&](float x, int j) -> uint32_t {   // invalid: 0xFFFFFFFF (> any T)
@@ -2623,7 +2623,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
     // candidate list capacity: smallest of {16, 32, 64} leaving a re-rank margin >= 4
     const int need = K - 1 + 4;
     const int KC = need <= 16 ? 16 : (need <= 32 ? 32 : 64);
-    if (K - 1 > kMaxKm1Wide) return hipErrorInvalidValue;
+    if (K - 1 > kMaxKm1Huge) return hipErrorInvalidValue;
     int margin = KC - (K - 1);
     if (margin > 8) margin = 8;
     int kc = K - 1 + margin;
@@ -2640,7 +2640,15 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
         const int kcw = min(K - 1 + 8, n - 1);
         prof_begin(GLL_K_SELECT, s);
 #define GLL_SELW(V, NPV)                                                                       \
-        launch_k(knn_select_wide_kernel<V, NPV>, grid, 256, 0, s, L.at<float>(ws, L.D2), L.ldD,  \
+        do {                                                                                   \
+            if (K - 1 > kMaxKm1Wide)                                                           \
+                GLL_SELW_(V, NPV, 512, kMaxKm1Huge, 5);                                        \
+            else                                                                               \
+                GLL_SELW_(V, NPV, 256, kMaxKm1Wide, 4);                                        \
+        } while (0)
+#define GLL_SELW_(V, NPV, CAP, KMX, TOP)                                                       \
+        launch_k(knn_select_wide_kernel<V, NPV, CAP, KMX, TOP>, grid, 256, 0, s,                 \
+                 L.at<float>(ws, L.D2), L.ldD,                                                 \
                  plane, X, n, L.d, K, kcw, eps_fixed, auto_eps ? 1 : 0, L.RCAP,                \
                  L.at<int32_t>(ws, L.knn_idx), L.at<float>(ws, L.knn_d2), L.at<float>(ws, L.eps), \
                  L.at<int32_t>(ws, L.rev_cnt), L.at<int32_t>(ws, L.rev_idx),                   \
@@ -2654,6 +2662,7 @@ hipError_t launch_select(const Layout& L, const Batch& bt, void* ws, const float
             else GLL_SELW(false, 1);
         }
 #undef GLL_SELW
+#undef GLL_SELW_
         prof_end(GLL_K_SELECT, s);
         return launch_status("knn.hip:launch_select(wide)");
     }

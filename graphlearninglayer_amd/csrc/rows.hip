@@ -111,8 +111,8 @@ __device__ __forceinline__ float yval(const TY* Y, int j, int C, int c) {
 // of their first 64 staged entries right after staging, so the loads overlap the sort and the
 // weights; the sums still run in sorted-column order (t_idx maps a sorted slot to its staged
 // entry), so results are unchanged.
-// FH: 64-entry halves of the forward list (K - 1 <= 64 FH): entry 64 h + lane of row i's kNN list
-// sits in lane `lane` of fi[h]; its valid entries are staged half after half.
+// FH: 64-entry parts of the forward list (K - 1 <= 64 FH): entry 64 h + lane of row i's kNN list
+// sits in lane `lane` of fi[h]; its valid entries are staged part after part.
 template <bool LDS, bool PRE, typename TY, int FH>
 __device__ __forceinline__ void build_row(const RowArgs& a, const TY* __restrict__ Y, int i,
                                           int start, const int (&fi)[FH], const float (&fd)[FH],
@@ -587,17 +587,23 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     // as fast or faster with global loads (6.5 -> 6.4 us).  XCD-contiguous numbering (R) measured
     // slower here even with the graph index taken once (NS B = 64 62 -> 66 us, FullySup B = 64
     // 116 -> 125 us, profiles/r02h_xcd_ab.txt).
-// (K - 1 > 64: the forward list in two 64-entry halves, FH = 2)
+// (K - 1 > 64: the forward list in 64-entry parts, FH = 2 up to K - 1 = 128, 4 up to 256)
+#define GLL_ROWS_FH(T, FHV)                                                                  \
+    do {                                                                                     \
+        if (bt.B == 1)                                                                       \
+            launch_k(row_build_kernel<T, true, false, false, FHV>, grid, 256, 0, s, a,       \
+                     static_cast<const T*>(Y), bt.y);                                        \
+        else                                                                                 \
+            launch_k(row_build_kernel<T, false, true, false, FHV>, grid, 256, 0, s, a,       \
+                     static_cast<const T*>(Y), bt.y);                                        \
+    } while (0)
 #define GLL_ROWS(T)                                                                          \
     do {                                                                                     \
-        if (L.K - 1 > kWave) {                                                               \
-            if (bt.B == 1)                                                                   \
-                launch_k(row_build_kernel<T, true, false, false, 2>, grid, 256, 0, s, a,     \
-                         static_cast<const T*>(Y), bt.y);                                    \
-            else                                                                             \
-                launch_k(row_build_kernel<T, false, true, false, 2>, grid, 256, 0, s, a,     \
-                         static_cast<const T*>(Y), bt.y);                                    \
-        } else if (pre)                                                                      \
+        if (L.K - 1 > 2 * kWave)                                                             \
+            GLL_ROWS_FH(T, 4);                                                               \
+        else if (L.K - 1 > kWave)                                                            \
+            GLL_ROWS_FH(T, 2);                                                               \
+        else if (pre)                                                                        \
             launch_k(row_build_kernel<T, true, false>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y);  \
         else if (bt.B == 1)                                                                  \
             launch_k(row_build_kernel<T, false, false>, grid, 256, 0, s, a, static_cast<const T*>(Y), bt.y); \
@@ -609,6 +615,7 @@ hipError_t launch_finalize(const Layout& L, const Batch& bt, void* ws, const voi
     else if (y_dtype == GLL_DT_I64) GLL_ROWS(int64_t);
     else return hipErrorInvalidValue;
 #undef GLL_ROWS
+#undef GLL_ROWS_FH
     prof_end(GLL_K_FINALIZE, s);
     return launch_status("rows.hip:launch_finalize");
 }

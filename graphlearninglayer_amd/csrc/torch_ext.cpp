@@ -39,7 +39,7 @@ namespace {
 using torch::autograd::variable_list;
 
 constexpr int64_t kDefaultK = 25;       // GLL.py:27
-constexpr int64_t kMaxK = 129;          // include/gll.h: 2 <= K <= 129
+constexpr int64_t kMaxK = 257;          // include/gll.h: 2 <= K <= 257
 constexpr int kMaxIter = 1000;
 constexpr float kRtol = 1e-6f;
 constexpr int kFlushEvery = 64;         // calls between status copies

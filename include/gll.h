@@ -103,7 +103,7 @@ typedef struct gll_problem {
     int32_t d;        /* feature dimension */
     int32_t base;     /* labeled rows = label_matrix.shape[0] (GLL.py:32) */
     int32_t C;        /* classes = label_matrix.shape[1] */
-    int32_t K;        /* neighbours incl. self, 2 <= K <= 129 (K >= n is clamped to n); the reference
+    int32_t K;        /* neighbours incl. self, 2 <= K <= 257 (K >= n is clamped to n); the reference
                        * hard-codes 25 (GLL.py:27) */
     int32_t max_iter; /* CG iteration cap per column; 0 => 1000 */
     float tau;        /* diagonal regulariser of Luu (GLL.py:48) */

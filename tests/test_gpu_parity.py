@@ -986,6 +986,28 @@ def test_balanced_cg_spill_path_matches_oracle(monkeypatch):
     assert O.rel_err(gr1, O.backward(st, g)) <= TOL
 
 
+def test_balanced_cg_vrm_clamp_at_wide_k_matches_oracle():
+    """Advisor (round 5): at k = 129 a U row may need ceil((5(K-1)+8)/8) = 81 virtual-row slots,
+    past the 63 the CG's 6-bit slot field holds (vr_max_per_row clamps), so long rows keep their
+    tail in the CSR.  Forcing the balanced kernel (GLL_FLAG_CG_VR, 10 virtual rows per thread)
+    at k = 129 runs the clamp and the spill path together; forward and adjoint against the
+    oracle."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
+    X, lab = synth(500, 500, 64, C=10, r=1.0, seed=6)
+    Y = one_hot(lab[:500])
+    g = seeded_gbar(500, 10, 5)
+    _lib.set_knob(_lib.KNOB_VR_RV, 10)
+    try:
+        U, gr = _fwd_bwd_c_abi(X, Y, 129, 0.07, 1.0, g, flags=_lib.FLAG_CG_VR)
+    finally:
+        _lib.set_knob(_lib.KNOB_VR_RV, 0)
+    ind = _gpu_knn(X, 129, 1.0)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, st = O.forward(X, Y, tau=0.07, epsilon=1.0, K=129, knn=(ind, None))
+    assert O.rel_err(U, Uo) <= TOL
+    assert O.rel_err(gr, O.backward(st, g)) <= TOL
+
+
 def _fwd_bwd_c_abi(X, Y, k, tau, eps, gbar, flags=0, bwd_flags=None, ws_fill=None):
     """gll_forward + gll_backward through ctypes with explicit problem flags: (U, grad_X).
     `bwd_flags`: the backward's own flags (default: the forward's); `ws_fill`: a byte value the
@@ -1567,10 +1589,12 @@ def test_batched_two_row_cg_ragged_and_hub_rows_match_oracle(m, k, eps):
 
 
 # ----------------------------------------------------------------------------------------
-# k past one candidate per lane (kMaxKm1 = 56 < K - 1 <= 128): knn_select_wide_kernel.  The
-# reference takes any k (the constant at GLL.py:27, knn_num in utils.py:574).
+# k past one candidate per lane (kMaxKm1 = 56 < K - 1 <= 256): knn_select_wide_kernel (256
+# candidate slots up to K - 1 = 128, 512 past it).  The reference takes any k (the constant at
+# GLL.py:27, knn_num in utils.py:574).
 # ----------------------------------------------------------------------------------------
-@pytest.mark.parametrize("k,eps", [(64, 1.0), (100, "auto"), (129, 1.0)])
+@pytest.mark.parametrize("k,eps", [(64, 1.0), (100, "auto"), (129, 1.0), (130, "auto"),
+                                   (200, 1.0), (257, "auto")])
 def test_wide_k_exact_knn_and_oracle(k, eps):
     """NS shape (500 + 500 x 512): the kNN lists are the exact float64 kNN, and U and grad_X
     match the float64 oracle on them (GLL.py:14-177)."""
@@ -1621,7 +1645,51 @@ def test_wide_k_batched_and_rescan():
     assert O.rel_err(grad, O.backward(st, gb)) < TOL
 
 
-@pytest.mark.parametrize("knn_num", [64, 100])
+@pytest.mark.parametrize("k", [100, 200])
+def test_wide_k_ties_past_the_candidate_slots(k):
+    """Advisor (round 5): more tied columns than the wide select's candidate slots (256 / 512):
+    a cluster of 600 exact duplicates, so the threshold scan's compaction overflows and the
+    full-row bisection for T' with ties in index order runs (GLL_ST_KNN_MERGE); the lists are
+    still the exact float64 kNN (ties by index) and U, grad_X the oracle's."""
+    from graphlearninglayer_amd import _lib
+    rng = np.random.default_rng(7)
+    n, d, base = 1400, 48, 200
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    X[600:1200] = X[599]     # 601 copies of one point
+    lab = np.arange(n) % 10
+    Y = np.eye(10, dtype=np.float32)[lab[:base]]
+    gb = rng.standard_normal((n - base, 10))
+    g = _gpu_knn(X, k, 1.0)
+    ind = g["knn_idx"].cpu().numpy()
+    assert int(g["status"][_lib.ST_KNN_MERGE].item()) > 0
+    assert O.knn_set_mismatch(X, ind, k) == []
+    U, grad = _run(X, Y, 0.07, 1.0, k, gb)
+    Uo, st = O.forward(X, Y, 0.07, 1.0, k, knn=(ind.astype(np.int64), None))
+    assert O.rel_err(U, Uo) < TOL
+    assert O.rel_err(grad, O.backward(st, gb)) < TOL
+
+
+@pytest.mark.parametrize("k,eps", [(100, 1.0), (200, "auto")])
+def test_wide_k_row_panels_match_whole_matrix(k, eps):
+    """Advisor (round 5): the wide select on the row-panel route (GLL_FLAG_KNN_PANEL: 1,024-row
+    panels, a ragged last one): bitwise the whole-matrix path, and the oracle."""
+    from graphlearninglayer_amd import _lib
+    from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
+    X, lab = synth(300, 2200, 64, C=10, r=1.0, seed=61)
+    Y = one_hot(lab[:300])
+    g = seeded_gbar(2200, 10, 62)
+    U0, gr0 = _fwd_bwd_c_abi(X, Y, k, 0.07, eps, g)
+    U1, gr1 = _fwd_bwd_c_abi(X, Y, k, 0.07, eps, g, flags=_lib.FLAG_KNN_PANEL)
+    np.testing.assert_array_equal(U0, U1)
+    np.testing.assert_array_equal(gr0, gr1)
+    ind = _gpu_knn(X, k, eps)["knn_idx"].cpu().numpy().astype(np.int64)
+    Uo, st = O.forward(X, Y, 0.07, eps, k, knn=(ind, None))
+    assert O.rel_err(U1, Uo) <= TOL
+    assert O.rel_err(gr1, O.backward(st, g)) <= TOL
+
+
+@pytest.mark.parametrize("knn_num", [64, 100, 200])
 def test_utils_laplace_wide_knn_num(knn_num):
     """utils.laplace with knn_num = 64 / 100 (utils.py:574) on 250 + 4,000 points: exact kNN
     on sampled rows and the oracle's solution."""

@@ -60,9 +60,32 @@ def test_workspace_bytes_and_validation():
     assert lib.gll_workspace_bytes(ct.byref(bad)) == 0
     wide_k = G.make_problem(1000, 512, 500, 10, 100, 0.07, 1.0)
     assert lib.gll_workspace_bytes(ct.byref(wide_k)) > nb   # the wide select (K - 1 <= 128)
-    big_k = G.make_problem(1000, 512, 500, 10, 130, 0.07, 1.0)
-    assert lib.gll_workspace_bytes(ct.byref(big_k)) == 0   # K - 1 > 128 (kMaxKm1Wide) unsupported
+    huge_k = G.make_problem(1000, 512, 500, 10, 257, 0.07, 1.0)
+    assert lib.gll_workspace_bytes(ct.byref(huge_k)) > 0    # K - 1 <= 256 (kMaxKm1Huge)
+    big_k = G.make_problem(1000, 512, 500, 10, 258, 0.07, 1.0)
+    assert lib.gll_workspace_bytes(ct.byref(big_k)) == 0   # K - 1 > 256 unsupported
     assert lib.gll_strerror(-2).decode().startswith("unsupported")
+
+
+@pytest.mark.parametrize("shape", [
+    # (n, d, base, C, K, cap in MB): NS, FullySup, stress, k = 129, the 60k utils.laplace graph
+    (1000, 512, 500, 10, 10, 14), (1500, 128, 250, 10, 25, 22), (8192, 1024, 4096, 10, 30, 370),
+    (2000, 64, 500, 10, 129, 84), (60250, 128, 250, 10, 50, 15500)])
+def test_workspace_bytes_bounded_per_row(shape):
+    """Advisor (round 5): the row slot width must not grow with the reverse-list capacity.  Past
+    the n x n distances (and the hi/lo Gram planes) a row costs the six slot arrays (24 B a slot,
+    Wcap = 5(K-1)+8 slots plus the 2(K-1) bump share), the reverse list (8 B x RCAP = 8(K-1)+8),
+    the overflow triples, the kNN lists and O(C) vectors -- nothing more."""
+    n, d, base, C, K, cap_mb = shape
+    lib = _lib.lib()
+    nb = lib.gll_workspace_bytes(ct.byref(G.make_problem(n, d, base, C, K, 0.07, 1.0)))
+    assert 0 < nb <= cap_mb * 1e6
+    ks = 2 if ((n + 63) // 64 <= 16 and 256 < d <= 512) else 1
+    dense = ks * n * ((n + 3) & ~3) * 4 + n * ((d + 63) // 64 * 64) * 4
+    km1 = K - 1
+    per_row = (24 * (7 * km1 + 8) + 8 * (8 * km1 + 8) + 12 * km1 + 8 * K + 16 * 24
+               + 48 * 63 + 24 * C + 64)
+    assert nb - dense <= n * per_row + 64 * 1024, (nb - dense) / n
 
 
 def test_every_launched_kernel_has_device_code():
@@ -172,17 +195,17 @@ def test_torch_extension_module_loads():
 
 
 def test_k_outside_the_supported_range_raises_a_clear_error():
-    """k (neighbours incl. self) must satisfy 2 <= min(k, n) <= 129 (include/gll.h): the Python
+    """k (neighbours incl. self) must satisfy 2 <= min(k, n) <= 257 (include/gll.h): the Python
     layer says so before anything reaches the device."""
     import torch
     from graphlearninglayer_amd import GLL
-    X = torch.zeros(200, 8)
+    X = torch.zeros(400, 8)
     Y = torch.zeros(10, 3)
-    for k in (1, 130, 150):
+    for k in (1, 258, 300):
         with pytest.raises(ValueError, match="2 <= min"):
             GLL.LaplaceLearningSparseHard.apply(X, Y, 0.0, 1.0, k)
     with pytest.raises(ValueError, match="2 <= min"):
-        GLL.device_graph(X, 140)
+        GLL.device_graph(X, 260)
 
 
 def test_product_library_reads_no_switch_but_debug():
