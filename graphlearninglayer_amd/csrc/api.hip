@@ -465,6 +465,13 @@ extern "C" int gll_trace_read_wg(int unit, unsigned long long* out) {
     }
 }
 
+namespace gll { void trace_read_fz(unsigned long long*); }
+extern "C" int gll_trace_read_fz(unsigned long long* out) {
+    (void)hipDeviceSynchronize();
+    gll::trace_read_fz(out);
+    return GLL_OK;
+}
+
 extern "C" int gll_trace_reset(int unit) {
     (void)hipDeviceSynchronize();
     switch (unit) {

@@ -33,6 +33,20 @@
 namespace gll {
 
 GLL_TRACE_UNIT(solve)
+#ifdef GLL_TRACE
+// fused backward, per gradient wave (row): [0] release seen, [1] w loaded + first coefficients,
+// [2] products done, [3] stored, [4] (row length) | (CU id << 16) | (XCC id << 24)
+static __device__ unsigned long long g_fz[5 * 4096];
+void trace_read_fz(unsigned long long* out) {
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fz), sizeof(g_fz));
+}
+#define GLL_FZ(slot, wv, val)                                                                  \
+    do {                                                                                       \
+        if (lane_id() == 0 && (wv) < 4096) g_fz[(slot) * 4096 + (wv)] = (val);                 \
+    } while (0)
+#else
+#define GLL_FZ(slot, wv, val) do {} while (0)
+#endif
 
 static constexpr size_t kLdsLimit = 160 * 1024;
 static constexpr size_t kLdsDyn = kLdsLimit - 1024;   // dynamic share, room for static LDS
@@ -1116,6 +1130,7 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
     const bool ok = s_ok != 0;
 #ifdef GLL_TRACE
     if (tr) g_trace[17] = __builtin_amdgcn_s_memrealtime();
+    GLL_FZ(0, i0, __builtin_amdgcn_s_memrealtime());
 #endif
 #pragma unroll
     for (int q = 0; q < NC; ++q)
@@ -1127,6 +1142,14 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
     for (int e0 = beg; e0 < end; e0 += kWave) {
         if (e0 != beg) edge_pre(e0 + lane, cj, we, pj);   // rows past 64 edges (hubs)
         const float cf = edge_coef(e0 + lane, cj, we, pj);
+#ifdef GLL_TRACE
+        if (e0 == beg) {
+            float cfo = cf;
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(cfo)::"memory");
+            if (cfo == 12345.f) g_trace[9] = 0;
+            GLL_FZ(1, i0, __builtin_amdgcn_s_memrealtime());
+        }
+#endif
         const int cnt = min(kWave, end - e0);
         for (int t0 = 0; t0 < cnt; t0 += EB) {
             float sv[EB];
@@ -1151,6 +1174,14 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
             }
         }
     }
+#ifdef GLL_TRACE
+    {
+        f32x4 ao = acc[0];
+        asm volatile("" : "+v"(ao));
+        if (ao.x == 12345.f) g_trace[9] = 0;
+        GLL_FZ(2, i0, __builtin_amdgcn_s_memrealtime());
+    }
+#endif
     if (live) {
         const float nanf_ = __builtin_nanf("");
         float* oi = out + size_t(i) * d;
@@ -1161,6 +1192,18 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
             if (k < d) __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(oi + k));
         }
     }
+#ifdef GLL_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    GLL_FZ(3, i0, __builtin_amdgcn_s_memrealtime());
+    {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        GLL_FZ(4, i0, (unsigned long long)(end - beg) | ((unsigned long long)((hw >> 8) & 0xffff) << 16) |
+                          ((unsigned long long)(xcc & 0xff) << 40));
+    }
+#endif
     __syncthreads();
 #ifdef GLL_TRACE
     if (tr) g_trace[18] = __builtin_amdgcn_s_memrealtime();

@@ -1,10 +1,24 @@
-"""Host model of the CG -> Chebyshev hybrid for the per-column solves (design aid, CPU only).
+"""Host model of Chebyshev variants of the per-column solves (design aid, CPU only; round 6).
 
-Builds Luu of the bench shapes with the oracle and counts matrix passes of
-  * Jacobi PCG (Chronopoulos-Gear, what cg_ell_kernel MODE 1 runs), rtol 1e-6, and
-  * k0 PCG iterations, Ritz bounds of the Lanczos matrix they define, then preconditioned
-    Chebyshev for a pass count computed from those bounds, one residual check, PCG after.
-    python tools/cheb_sim.py [ns|fullysup] [k0] [lo_margin] [hi_margin] [safety]
+The per-column CG (cg_ell_kernel) is bound by each workgroup's iteration chain: a publish
+barrier, the LDS gathers, then a fused three-value reduction and the step sizes
+(profiles/r05e_trace_sell_b64.txt, B = 64 NS, iteration 3 in shader cycles: update+store ~190,
+publish barrier ~160, spmv+dots ~1,800, reduce ~480, alpha/beta+p,s ~600 -> ~3,300).
+Chebyshev iteration needs no reduction -- only the spectrum's bounds -- so its iteration is
+priced here at ~2,050 cycles (no reduce, no step sizes) plus ~500 per residual check.  This
+script counts iterations and prices three schemes against Jacobi PCG (what MODE 1 runs) on
+Luu of the bench shapes (oracle graphs, 4 seeds, 10 columns, rtol 1e-6, the slowest column
+of each solve):
+  hybrid   k0 PCG iterations, Ritz bounds of their Lanczos matrix, then Chebyshev with a
+           residual check every ck iterations (the forward: nothing is known in advance);
+  adjoint  Chebyshev from x = 0 with the bounds of the FORWARD solve's Lanczos matrices
+           (min / max over its columns, with margins), checks every ck iterations;
+  and the same adjoint scheme under the Neumann-1 preconditioner (MODE 3, single graphs).
+    python tools/cheb_sim.py [ns|fullysup]
+Result (NS, round 6): hybrid 1.00-1.41x the PCG cost (never cheaper); adjoint 0.76-0.82x
+with Jacobi (12-15 iterations against 11-12) but 8-9 iterations against 6-7 with Neumann-1
+(no gain).  So only the batched adjoint launch could gain (~2.5 us of a 660 us B = 64 call):
+not built.
 """
 import sys
 
@@ -14,35 +28,35 @@ sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth  # noqa: E402
 from oracle import gll_oracle as O  # noqa: E402
 
+C_CG, C_CHEB, C_CHECK, C_EIG = 3300, 2050, 500, 300   # shader cycles (see the docstring)
 
-def pcg(A, Dinv, b, rtol, maxit=1000, x=None, r=None):
+
+def pcg(A, Minv, b, rtol, maxit=1000, x=None, r=None):
     x = np.zeros_like(b) if x is None else x.copy()
     r = b.copy() if r is None else r.copy()
     bb = b @ b
-    z = Dinv * r
+    z = Minv(r)
     p = z.copy()
     rz = r @ z
     al, be = [], []
     it = 0
-    passes = 0
     while r @ r > rtol * rtol * bb and it < maxit:
         s = A @ p
-        passes += 1
         a = rz / (p @ s)
         x += a * p
         r -= a * s
-        z = Dinv * r
+        z = Minv(r)
         rz2 = r @ z
-        b_ = rz2 / rz
         al.append(a)
-        be.append(b_)
-        p = z + b_ * p
+        be.append(rz2 / rz)
+        p = z + (rz2 / rz) * p
         rz = rz2
         it += 1
-    return x, r, it, passes, al, be
+    return x, r, it, al, be
 
 
 def ritz(al, be):
+    """Extreme eigenvalues of the Lanczos matrix PCG's coefficients define."""
     k = len(al)
     T = np.zeros((k, k))
     for j in range(k):
@@ -53,68 +67,95 @@ def ritz(al, be):
     return ev[0], ev[-1]
 
 
-def hybrid(A, Dinv, b, rtol, k0, lom, him, safety):
-    x, r, it, passes, al, be = pcg(A, Dinv, b, rtol, maxit=k0)
-    if r @ r <= rtol * rtol * (b @ b):
-        return passes, 0, 0
-    lmin, lmax = ritz(al, be)
-    lo = lmin * lom
-    # lambda_max(D^-1 A) <= 2 - lambda_min(D^-1 A): D^-1 A = I - D^-1 N with D^-1 N >= 0, whose
-    # most negative eigenvalue is >= -rho(D^-1 N) = lambda_min - 1 (Perron); valid when lo is
-    hi = max(2.0 - lo, lmax * him) if him > 0 else 2.0 - lo
+def chebyshev(A, Minv, b, rtol, lo, hi, ck, x=None, r=None, cap=300):
+    """Preconditioned Chebyshev iteration on [lo, hi]; (iterations, checks) to rtol."""
+    x = np.zeros_like(b) if x is None else x
+    r = b.copy() if r is None else r
+    tol2 = rtol * rtol * (b @ b)
     th, de = (hi + lo) / 2, (hi - lo) / 2
     sg = th / de
-    ratio = np.sqrt((r @ r) / (rtol * rtol * (b @ b))) * safety
-    N = int(np.ceil(np.arccosh(ratio) / np.arccosh(sg)))
     rho = 1 / sg
-    d = Dinv * r / th
-    for _ in range(N):
+    d = Minv(r) / th
+    n = checks = 0
+    while n < cap:
         w = A @ d
-        passes += 1
+        n += 1
         x += d
         r -= w
         rn = 1 / (2 * sg - rho)
-        d = rn * rho * d + (2 * rn / de) * (Dinv * r)
+        d = rn * rho * d + (2 * rn / de) * Minv(r)
         rho = rn
-    extra = 0
-    if r @ r > rtol * rtol * (b @ b):
-        x, r, it2, p2, _, _ = pcg(A, Dinv, b, rtol, x=x, r=r)
-        passes += p2
-        extra = p2
-    return passes, N, extra
+        if n % ck == 0:
+            checks += 1
+            if r @ r <= tol2:
+                break
+    return n, checks
 
 
-def main():
-    cfg = sys.argv[1] if len(sys.argv) > 1 else "ns"
-    k0 = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    lom = float(sys.argv[3]) if len(sys.argv) > 3 else 0.9
-    him = float(sys.argv[4]) if len(sys.argv) > 4 else 1.05
-    safety = float(sys.argv[5]) if len(sys.argv) > 5 else 2.0
+def graphs(cfg, seeds=4):
     c = CONFIGS[cfg]
-    tot = [0, 0, 0]
-    for seed in range(4):
+    for seed in range(seeds):
         X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=seed)
         Y = one_hot(lab[: c["base"]])
         U, st = O.forward(X, Y, 0.07, 1.0, c["k"])
         A = st.Luu.tocsr()
-        Dinv = 1 / A.diagonal()
-        rhs = A @ U
-        g = seeded_gbar(c["batch"], 10, 1234 + seed)
-        for name, B in (("fwd", rhs), ("bwd", g)):
-            cg_p, hy_p, ns, ex = [], [], [], []
-            for col in range(B.shape[1]):
-                b = B[:, col]
-                cg_p.append(pcg(A, Dinv, b, 1e-6)[3])
-                p, N, e = hybrid(A, Dinv, b, 1e-6, k0, lom, him, safety)
-                hy_p.append(p)
-                ns.append(N)
-                ex.append(e)
-            tot[0] += max(cg_p)
-            tot[1] += max(hy_p)
-            tot[2] += max(ex) > 0
-            print(f"seed {seed} {name}: CG passes max {max(cg_p)}  hybrid max {max(hy_p)} "
-                  f"(cheb {min(ns)}-{max(ns)}, fallback cols {sum(e > 0 for e in ex)})")
-    print(f"total CG {tot[0]}  hybrid {tot[1]}  solves with fallback {tot[2]}")
+        Di = 1 / A.diagonal()
+        N = A.copy()
+        N.setdiag(0)
+        N = -N
+        yield seed, A, Di, N, A @ U, seeded_gbar(c["batch"], 10, 1234 + seed)
+
+
+def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "ns"
+    print("== forward hybrid (k0 PCG, Ritz bounds, Chebyshev with checks), Jacobi")
+    for k0, lom, ck, him in [(3, 0.9, 3, 1.1), (4, 0.9, 3, 1.1), (5, 0.95, 3, 1.05)]:
+        tot_h = tot_cg = 0
+        for seed, A, Di, N, rhs, g in graphs(cfg):
+            Minv = lambda r: Di * r   # noqa: E731
+            for B in (rhs, g):
+                hs, cs = [], []
+                for col in range(B.shape[1]):
+                    b = B[:, col]
+                    _, _, itc, _, _ = pcg(A, Minv, b, 1e-6)
+                    cs.append(itc * C_CG)
+                    x, r, it, al, be = pcg(A, Minv, b, 1e-6, maxit=k0)
+                    if r @ r <= 1e-12 * (b @ b):
+                        hs.append(it * C_CG)
+                        continue
+                    lmin, lmax = ritz(al, be)
+                    n, chk = chebyshev(A, Minv, b, 1e-6, lmin * lom, lmax * him, ck, x, r)
+                    hs.append(it * C_CG + C_EIG + n * C_CHEB + chk * C_CHECK)
+                tot_h += max(hs)
+                tot_cg += max(cs)
+        print(f"  k0 {k0} lo x{lom} hi x{him} check/{ck}: cost vs PCG {tot_h / tot_cg:.3f}")
+    for name in ("jacobi", "neumann-1"):
+        print(f"== adjoint Chebyshev with the forward's Ritz bounds, {name}")
+        for lom, him, ck in [(0.95, 1.05, 3), (0.97, 1.02, 2)]:
+            its_cg, its_ch, cost_r = [], [], []
+            for seed, A, Di, N, rhs, g in graphs(cfg):
+                if name == "jacobi":
+                    Minv = lambda r: Di * r   # noqa: E731
+                else:
+                    Minv = lambda r: Di * r + Di * (N @ (Di * r))   # noqa: E731
+                los, his = [], []
+                for col in range(rhs.shape[1]):
+                    *_, al, be = pcg(A, Minv, rhs[:, col], 1e-6)
+                    lmin, lmax = ritz(al, be)
+                    los.append(lmin)
+                    his.append(lmax)
+                lo, hi = min(los) * lom, max(his) * him
+                cg = max(pcg(A, Minv, g[:, col], 1e-6)[2] for col in range(g.shape[1]))
+                ch = [chebyshev(A, Minv, g[:, col], 1e-6, lo, hi, ck) for col in range(g.shape[1])]
+                n = max(c[0] for c in ch)
+                chk = max(c[1] for c in ch)
+                its_cg.append(cg)
+                its_ch.append(n)
+                cost_r.append((n * C_CHEB + chk * C_CHECK) / (cg * C_CG))
+            print(f"  lo x{lom} hi x{him} check/{ck}: PCG iterations {its_cg}, Chebyshev "
+                  f"{its_ch}, cost vs PCG {np.mean(cost_r):.3f}"
+                  + ("  (Neumann iterations cost ~0.74 of a PCG one: two gathers each)"
+                     if name != "jacobi" else ""))
 
 
 if __name__ == "__main__":
