@@ -52,7 +52,7 @@ def _load_ext():
         from . import _gll_torch
     except ImportError as e:
         raise ImportError("graphlearninglayer_amd: _gll_torch.so is missing or does not load "
-                          "(build it: python -m graphlearninglayer_amd.build). There is no "
+                          "(build it: python graphlearninglayer_amd/build.py). There is no "
                           f"CPU fallback. ({e})") from e
     return _gll_torch
 

@@ -116,7 +116,7 @@ def lib():
                 if not os.path.exists(LIB_PATH):
                     raise RuntimeError(
                         f"{LIB_PATH} is missing: build the HIP extension first "
-                        "(python -m graphlearninglayer_amd.build). There is no CPU fallback.")
+                        "(python graphlearninglayer_amd/build.py). There is no CPU fallback.")
                 _lib = _declare(ct.CDLL(LIB_PATH))
     return _lib
 

@@ -1,6 +1,8 @@
 """Build libgll.so (HIP kernels + C ABI) for gfx950 with hipcc, in-tree.
 
-    python -m graphlearninglayer_amd.build [--force] [--verbose]
+    python graphlearninglayer_amd/build.py [--force] [--verbose] [--trace] [--digest]
+    (or python -m graphlearninglayer_amd.build once the package imports, i.e. after a build:
+    the package refuses to import without its .so files -- there is no CPU fallback)
 
 The shared library lands next to this file so it travels to the GPU box with the repo
 snapshot (it is git-ignored).  Each translation unit is compiled separately (in parallel)
