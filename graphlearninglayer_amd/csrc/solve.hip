@@ -1029,8 +1029,7 @@ template <int NT, int S, typename TB, int ND>
 __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs a,
                                                            const float* __restrict__ X,
                                                            float* __restrict__ out,
-                                                           unsigned* fsync, int32_t* st_failed,
-                                                           int lds_rows) {
+                                                           unsigned* fsync, int32_t* st_failed) {
     const int C = c.C;
     if (int(blockIdx.x) < C) {
         cg_ell_body<NT, 1, S, TB, 3>(int2{int(blockIdx.x), 0}, fsync, c.m, C, c.base,
@@ -1107,34 +1106,6 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
 #pragma unroll
         for (int q = 0; q < ND; ++q) v[u][q] = load4_raw<true>(xj, 4 * lane + 4 * kWave * q, d);
     }
-    // Neighbour rows past the EB held in registers (the first 64 edges of a row) go to LDS by
-    // LDS-DMA before the wait, so no row waits for a second or third batch of gathers after the
-    // release (round 6: those rows -- 33-41 edges at NS -- were the last to leave, 5.4 us after
-    // the release against 2.3 for the median row, profiles/r06b_fused_tail.txt).  The launch's
-    // dynamic LDS (sized for the CG role, unused here) is dealt to the block's waves by demand,
-    // in wave order; rows past it load after the release as before.  Same values, same order:
-    // the sums are unchanged.
-    extern __shared__ __attribute__((aligned(16))) float smem_g[];
-    __shared__ int s_need[NT / kWave];
-    const int wv = threadIdx.x >> 6;
-    const int need = live && cnt0 > EB ? cnt0 - EB : 0;
-    if (lane == 0) s_need[wv] = need;
-    __syncthreads();
-    int before = 0;
-    for (int w = 0; w < wv; ++w) before += s_need[w];
-    const int np = max(0, min(lds_rows - before, need));   // rows this wave holds in LDS
-    char* lrow = reinterpret_cast<char*>(smem_g) + size_t(before) * ND * kWave * 16;
-    for (int sl = 0; sl < np; ++sl) {
-        const float* xj = X + size_t(readlane_i(cj, EB + sl)) * d;
-#pragma unroll
-        for (int q = 0; q < ND; ++q) {
-            const int k = 4 * lane + 4 * kWave * q;
-            __builtin_amdgcn_global_load_lds(xj + (k < d ? k : 0),
-                                             (__attribute__((address_space(3))) void*)(
-                                                 lrow + size_t(sl * ND + q) * kWave * 16),
-                                             16, 0, 0);
-        }
-    }
     // ---- wait for the C column solves (bounded: a lost solve surfaces as NaN + status)
     if (threadIdx.x == 0) {
         // a workspace whose previous fused backward lost a solve stays poisoned (its counter may
@@ -1161,8 +1132,6 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
     if (tr) g_trace[17] = __builtin_amdgcn_s_memrealtime();
     GLL_FZ(0, i0, __builtin_amdgcn_s_memrealtime());
 #endif
-    // this wave's LDS-DMA rows landed (issued ~the whole solve ago): vmcnt counts them
-    if (np > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int q = 0; q < NC; ++q)
         wi[q] = __builtin_bit_cast(
@@ -1188,18 +1157,9 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
 #pragma unroll
                 for (int u = 0; u < EB; ++u) {
                     const int t = t0 + u < cnt ? t0 + u : t0;
-                    const int sl = t - EB;   // its LDS slot (first 64 edges only)
-                    if (e0 == beg && sl < np) {
+                    const float* xj = X + size_t(readlane_i(cj, t)) * d;
 #pragma unroll
-                        for (int q = 0; q < ND; ++q)
-                            v[u][q] = *reinterpret_cast<const f32x4*>(
-                                lrow + size_t(sl * ND + q) * kWave * 16 + 16 * lane);
-                    } else {
-                        const float* xj = X + size_t(readlane_i(cj, t)) * d;
-#pragma unroll
-                        for (int q = 0; q < ND; ++q)
-                            v[u][q] = load4_raw<true>(xj, 4 * lane + 4 * kWave * q, d);
-                    }
+                    for (int q = 0; q < ND; ++q) v[u][q] = load4_raw<true>(xj, 4 * lane + 4 * kWave * q, d);
                 }
             }
 #pragma unroll
@@ -1314,10 +1274,8 @@ static hipError_t run_fused(const Layout& L, void* ws, const TB* b, const float*
     c.ell = L.at<int4>(ws, L.ell);
     const EdgeArgs a = make_edge_args(L, 0, ws, eps_fixed);
     prof_begin(GLL_K_BWD, s);
-    // the gradient role's neighbour rows in the same dynamic LDS (ND x 1 KiB each)
-    const int lds_rows = int(lds / (size_t(ND) * kWave * 16));
     launch_k(fn, dim3(unsigned(G)), NT, lds, s, c, a, X, gradX, L.at<unsigned>(ws, L.fsync),
-             st_failed, lds_rows);
+             st_failed);
     prof_end(GLL_K_BWD, s);
     return launch_status("solve.hip:run_fused");
 }
