@@ -201,6 +201,14 @@ __device__ __forceinline__ float rhs_at(const void* b, int dt, size_t i) {
 // while every other workgroup leaves without writing.  It depends on no other workgroup, so it
 // always completes; the solve is slower (one CU) and GLL_ST_GRID_RESCUED counts it.
 // ---------------------------------------------------------------------------------------
+// The solution stores of the grid kernels: write-through (see rescued()).
+__device__ __forceinline__ void st_out(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_out(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int NT>
 __device__ float rescue_sum(float v, float* red) {
     v = wave_sum_dpp(v);
@@ -217,8 +225,22 @@ template <class Mat, int NT>
 __device__ void rescue_solve(const Mat& A, int m, int C, const void* b, int b_dtype, float rtol,
                              float atol, int max_iter, double* out64, float* out32,
                              float* scr /* 5 m floats */, int32_t* st_iters,
-                             int32_t* st_nonconv, int32_t* st_rescued) {
+                             int32_t* st_nonconv, int32_t* st_rescued, unsigned* begun,
+                             unsigned* finished) {
     __shared__ float red[NT / kWave];
+    // every registered writer of the failed solve has counted out (bounded: they are resident
+    // and past their last barrier) before this workgroup writes its first row
+    auto wait_writers = [&]() {
+        if (threadIdx.x == 0) {
+            const unsigned long long t0 = wall_ticks();
+            while (__hip_atomic_load(finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                       __hip_atomic_load(begun, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
+                   wall_ticks() - t0 < kWaitTicks)
+                __builtin_amdgcn_s_sleep(2);
+        }
+        __syncthreads();
+    };
+    bool waited = false;
     float *X_ = scr, *R_ = scr + m, *P_ = scr + 2 * size_t(m), *Q_ = scr + 3 * size_t(m),
           *M_ = scr + 4 * size_t(m);
     int it_max = 0, nonconv = 0;
@@ -278,10 +300,14 @@ __device__ void rescue_solve(const Mat& A, int m, int C, const void* b, int b_dt
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
+        if (!waited) {
+            wait_writers();
+            waited = true;
+        }
         for (int u = threadIdx.x; u < m; u += NT) {
             const float xv = ld_shared(X_ + u);
-            if (out64) out64[size_t(u) * C + c] = double(xv);
-            if (out32) out32[size_t(u) * C + c] = xv;
+            if (out64) st_out(out64 + size_t(u) * C + c, double(xv));
+            if (out32) st_out(out32 + size_t(u) * C + c, xv);
         }
         it_max = it > it_max ? it : it_max;
         nonconv += conv ? 0 : 1;
@@ -297,16 +323,28 @@ __device__ void rescue_solve(const Mat& A, int m, int C, const void* b, int b_dt
 // After a grid kernel's loop: true when this workgroup must write nothing because a barrier
 // failed (it rescued the solve, or another workgroup does).  A workgroup whose own barriers all
 // completed can still be in that case: a late arrival completes the final barrier just after
-// another workgroup timed out on it and claimed the rescue.  Such a workgroup reads the failure
-// word and leaves the solution to the rescuer, so U is never a mix of the two solves.  (A
-// workgroup that read the word just before the timeout still writes: a rescued solve -- counted
-// in GLL_ST_GRID_RESCUED -- is correct to the CG tolerance but not bitwise reproducible.)
+// another workgroup timed out on it and claimed the rescue.  Writers register before they read
+// the failure word (`begun`, a returning atomic at the coherence point, so the read is issued
+// after it), write their rows write-through (sc1: no dirty copy in their XCD's L2 can be written
+// back over the rescue later) and then count themselves out (`finished`; a writer that reads the
+// failure word set counts out without writing).  The rescuer solves, then waits until every
+// registered writer has counted out and writes every row: a writer registering after that saw
+// the failure word (set before the rescuer claimed) and wrote nothing.  So U is the rescue
+// solution alone, never a mix of two solves (advisor, round 5).
 template <class Mat, int NT, class Args>
-__device__ bool rescued(bool ok, unsigned* fail_word, unsigned* rescue_word, const Mat& A,
-                        const Args& a, float* scr, int* s_flag) {
+__device__ bool rescued(bool ok, unsigned* fail_word, unsigned* rescue_word, unsigned* begun,
+                        unsigned* finished, const Mat& A, const Args& a, float* scr, int* s_flag) {
     if (ok) {
-        if (threadIdx.x == 0)
-            *s_flag = __hip_atomic_load(fail_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        if (threadIdx.x == 0) {
+            (void)__hip_atomic_fetch_add(begun, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const bool failed =
+                __hip_atomic_load(fail_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+            if (failed)
+                (void)__hip_atomic_fetch_add(finished, 1u, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+            *s_flag = failed;
+        }
         __syncthreads();
         return *s_flag != 0;
     }
@@ -316,8 +354,17 @@ __device__ bool rescued(bool ok, unsigned* fail_word, unsigned* rescue_word, con
     __syncthreads();
     if (*s_flag)
         rescue_solve<Mat, NT>(A, a.m, a.C, a.b, a.b_dtype, a.rtol, a.atol, a.max_iter, a.out64,
-                              a.out32, scr, a.st_iters, a.st_nonconv, a.st_rescued);
+                              a.out32, scr, a.st_iters, a.st_nonconv, a.st_rescued, begun,
+                              finished);
     return true;
+}
+
+// A writer's end of the protocol above: its sc1 stores are performed, then it counts out.
+__device__ __forceinline__ void writer_done(unsigned* finished) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        (void)__hip_atomic_fetch_add(finished, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ f32x4 quad_of(const float* s, int q) {
@@ -531,7 +578,9 @@ __global__ __launch_bounds__(kGT) void cg_grid_classic_kernel(Mat A, GridCgArgs 
     GLL_TRACE_PT(1);
     // a failed grid barrier (a workgroup never arrived within ~1 s): one workgroup solves the
     // system alone (rescue_solve), the others write nothing
-    if (rescued<Mat, kGT>(ok, a.sync + 1, a.sync + 2, A, a, a.rescue, &s_ok)) return;
+    if (rescued<Mat, kGT>(ok, a.sync + 1, a.sync + 2, a.sync + 3, a.sync + 4, A, a, a.rescue,
+                          &s_ok))
+        return;
 #pragma unroll
     for (int k = 0; k < RPG; ++k) {
         const int u = r0 + grp + k * NG;
@@ -541,11 +590,12 @@ __global__ __launch_bounds__(kGT) void cg_grid_classic_kernel(Mat A, GridCgArgs 
             const int c = 4 * li + t;
             if (c < C) {
                 const size_t i = size_t(u) * C + c;
-                if (a.out64) a.out64[i] = double(x[k][t]);
-                if (a.out32) a.out32[i] = x[k][t];
+                if (a.out64) st_out(a.out64 + i, double(x[k][t]));
+                if (a.out32) st_out(a.out32 + i, x[k][t]);
             }
         }
     }
+    writer_done(a.sync + 4);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         int nonconv = 0;
         for (int c = 0; c < C; ++c) nonconv += s_active[c] != 0 ? 1 : 0;
@@ -561,14 +611,16 @@ constexpr int kMaxG = 256;            // workgroups of one pipelined solve (<= o
 constexpr int kGvMaxRows = 512;       // rows per workgroup: NG x RPG <= 64 x 8
 constexpr int kSyncLine = 32;         // words per sync word (one 128-B line each)
 // sync lines: [0, 8) group arrival counters, 8 top counter, 9 failure, 10 rescue, [11, 19)
-// release words (one per group), 19 exit counter
+// release words (one per group), 19 exit counter, 20 / 21 writers registered / counted out
+// (rescued())
 #ifndef GLL_GV_GROUPS
 #define GLL_GV_GROUPS 8
 #endif
 constexpr int kGvGroups = GLL_GV_GROUPS;   // arrival groups of the two-level barrier
 constexpr int kSyncTop = kGvGroups, kSyncFail = kGvGroups + 1, kSyncRescue = kGvGroups + 2,
-              kSyncRel = kGvGroups + 3, kSyncExit = 2 * kGvGroups + 3;
-constexpr int kSyncWords = (2 * kGvGroups + 4) * kSyncLine;
+              kSyncRel = kGvGroups + 3, kSyncExit = 2 * kGvGroups + 3,
+              kSyncBegun = 2 * kGvGroups + 4, kSyncFinished = 2 * kGvGroups + 5;
+constexpr int kSyncWords = (2 * kGvGroups + 6) * kSyncLine;
 static_assert(kSyncWords <= kGridSyncWords, "gll_internal.h kGridSyncWords (row_build zeroes them)");
 
 struct GvArgs {
@@ -1067,7 +1119,8 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
     GLL_TRACE_PT(10);
     // a failed grid barrier (a workgroup never arrived within ~1 s): one workgroup solves the
     // system alone (rescue_solve), the others write nothing
-    if (!rescued<Mat, NT>(ok, a.sync + kSyncFail * kSyncLine, a.sync + kSyncRescue * kSyncLine, A,
+    if (!rescued<Mat, NT>(ok, a.sync + kSyncFail * kSyncLine, a.sync + kSyncRescue * kSyncLine,
+                          a.sync + kSyncBegun * kSyncLine, a.sync + kSyncFinished * kSyncLine, A,
                           a, a.rescue, &s_ok)) {
 #pragma unroll
         for (int k = 0; k < RPG; ++k) {
@@ -1078,11 +1131,12 @@ __global__ __launch_bounds__(NT) void cg_gv_kernel(Mat A, GvArgs a) {
                 const int c = 4 * li + t;
                 if (c < C) {
                     const size_t i = size_t(uu) * C + c;
-                    if (a.out64) a.out64[i] = double(x[k][t]);
-                    if (a.out32) a.out32[i] = x[k][t];
+                    if (a.out64) st_out(a.out64 + i, double(x[k][t]));
+                    if (a.out32) st_out(a.out32 + i, x[k][t]);
                 }
             }
         }
+        writer_done(a.sync + kSyncFinished * kSyncLine);
         const int nonconv = __popcll(__ballot(lane < C && act_c != 0));
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             if (a.st_iters) atomicMax(a.st_iters, it);
@@ -1141,12 +1195,12 @@ static hipError_t launch_grid(const Mat& A, GridCgArgs a, int G, float* ws, hipS
     if (G > 1024 || G > coresident_capacity<Mat, LPR, RPG>())   // partials hold 1024 workgroups
         return hipErrorCooperativeLaunchTooLarge;
     a.Cp = (a.C + 3) & ~3;
-    a.sync = reinterpret_cast<unsigned*>(ws);          // 16-B block at the region's start
+    a.sync = reinterpret_cast<unsigned*>(ws);          // 32-B block at the region's start
     a.Pbuf = ws + 64;                                   // 256-B aligned: 16-B buffer accesses
     a.Zbuf = a.Pbuf + size_t(2) * a.m * a.Cp;
     a.part = a.Zbuf + size_t(a.m) * a.Cp;
     a.rescue = ws + rescue_offset(a.m, a.C);
-    hipError_t e = hipMemsetAsync(a.sync, 0, 16, s);
+    hipError_t e = hipMemsetAsync(a.sync, 0, 32, s);   // barrier, fail, rescue, writers in/out
     if (e != hipSuccess) return e;
     return launch_persistent(cg_grid_classic_kernel<Mat, LPR, RPG>, G, kGT, 0, s,
                              "gridcg.hip:launch_grid", A, a);

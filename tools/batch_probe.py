@@ -12,7 +12,8 @@ from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth  #
 
 cfg = os.environ.get("PROBE_CFG", "ns")
 c = CONFIGS[cfg]
-eps = float(os.environ.get("PROBE_EPS", "1.0"))
+eps = os.environ.get("PROBE_EPS", "1.0")
+eps = eps if eps == "auto" else float(eps)
 dev = torch.device("cuda", 0)
 names = [_lib.kernel_name(q) for q in range(_lib.K_COUNT)]
 Xs, Ys = [], []

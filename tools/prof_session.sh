@@ -17,6 +17,7 @@ cmd_for() {   # the workload of a cfg: the bench's single-graph step, or the bat
     stress) echo "python3 $R/bench.py --config stress --steps 10 --warmup 3 --cpu-seconds 0 --no-profile --batch 0";;
     ns_b64) echo "PROBE_B=64 PROBE_CFG=ns python3 $R/tools/batch_probe.py";;
     fullysup_b64) echo "PROBE_B=64 PROBE_CFG=fullysup python3 $R/tools/batch_probe.py";;
+    stress_b64) echo "PROBE_B=64 PROBE_CFG=stress PROBE_EPS=auto python3 $R/tools/batch_probe.py";;
   esac
 }
 MF="--pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv"
