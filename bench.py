@@ -240,19 +240,24 @@ def rocprof_stats(config):
 
 
 def rocprof_avg_us(rel, kernel):
-    """Mean rocprof duration (us) over every launch of the symbols of C-ABI kernel `kernel`
-    in a committed kernel_stats CSV."""
+    """Mean rocprof duration (us) per C-ABI launch of `kernel` in a committed kernel_stats CSV:
+    the summed durations of its device symbols over the calls of the first symbol present (the
+    Gram id spans gram_split + the main GEMM + its tail; the events bracket that whole span)."""
     import csv
     if rel is None:
         return None
-    tot_ns, calls = 0.0, 0
+    tot_ns, calls = 0.0, {}
+    syms = PMC_SYMBOLS[kernel] + (["gram_split_kernel"] if kernel == "gram_d2_kernel" else [])
     with open(os.path.join(ROOT, rel)) as f:
         for row in csv.DictReader(f):
             name = row["Name"]
-            if any(f"::{sym}<" in name or f"::{sym}(" in name for sym in PMC_SYMBOLS[kernel]):
-                tot_ns += float(row["TotalDurationNs"])
-                calls += int(row["Calls"])
-    return round(tot_ns / calls / 1e3, 3) if calls else None
+            for sym in syms:
+                if f"::{sym}<" in name or f"::{sym}(" in name:
+                    tot_ns += float(row["TotalDurationNs"])
+                    calls[sym] = calls.get(sym, 0) + int(row["Calls"])
+                    break
+    main = next((calls[sym] for sym in PMC_SYMBOLS[kernel] if sym in calls), 0)
+    return round(tot_ns / main / 1e3, 3) if main else None
 
 
 def gram_mfma_pmc(config):
