@@ -731,10 +731,14 @@ __device__ __forceinline__ void supertile_tile(int t, int T, int& bi, int& bj) {
 
 // One-dimensional grid over B graphs x T (T + 1) / 2 tiles: xcd_tile deals each XCD a
 // contiguous run of the graph-major sequence, so a batch's graphs are XCD-local too.
-// t0 >= 0 (the tail of a 256-tile launch, launch_gram): block 4 j + s computes 128-subtile s of
-// 256-tile t0 + j in gram_pk2_kernel's sequence (T2 = ceil(T / 2) blocks a side); subtiles below
-// a diagonal 256-tile's diagonal or past n return at once.
-template <bool H>
+// t0 >= 0 (the tail of a 256-tile launch, launch_gram): with Q = 256 / TS, block Q^2 j + s
+// computes TS-subtile s of 256-tile t0 + j in gram_pk2_kernel's sequence (T2 = ceil(T / Q)
+// blocks a side, T counted in TS-tiles); subtiles below a diagonal 256-tile's diagonal or past
+// n return at once.  TS = 64 (round 6): the tail's 16 256-tiles at stress become 256 workgroups,
+// one per CU, instead of 64 128-subtiles on a quarter of the chip; each wave then holds one
+// 32 x 32 accumulator.  Every element still sums the same MFMA sequence over k: D2 is bitwise
+// the same for any TS.
+template <bool H, int TS>
 __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__ Ph,
                                                       const __bf16* __restrict__ Pl,
                                                       const float* __restrict__ nrm, int n,
@@ -749,13 +753,14 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
         g = idx / NT;
         supertile_tile(idx - g * NT, T, bi, bj);
     } else {
-        const int T2 = (T + 1) / 2, NT2 = T2 * (T2 + 1) / 2;
-        const int idx2 = t0 + int(blockIdx.x >> 2), sub = int(blockIdx.x & 3);
+        constexpr int Q = 256 / TS;
+        const int T2 = (T + Q - 1) / Q, NT2 = T2 * (T2 + 1) / 2;
+        const int idx2 = t0 + int(blockIdx.x) / (Q * Q), sub = int(blockIdx.x) % (Q * Q);
         int b2i, b2j;
         g = idx2 / NT2;
         supertile_tile(idx2 - g * NT2, T2, b2i, b2j);
-        bi = 2 * b2i + (sub >> 1);
-        bj = 2 * b2j + (sub & 1);
+        bi = Q * b2i + sub / Q;
+        bj = Q * b2j + sub % Q;
         if (bi > bj || bj >= T) return;   // whole workgroup, before any barrier
     }
     {
@@ -766,39 +771,43 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
         D2 = reinterpret_cast<float*>(reinterpret_cast<char*>(D2) + off);
         d2s = reinterpret_cast<float*>(reinterpret_cast<char*>(d2s) + off);
     }
-    constexpr int kTP = 128 * kPK;                                  // bf16 per tile plane
-    __shared__ __attribute__((aligned(16))) __bf16 sm[2 * 4 * kTP];  // 128 KiB: [buf][plane]
+    static_assert(TS == 128 || TS == 64, "128- or 64-row tiles");
+    constexpr int MA = TS / 64;                // 32 x 32 accumulators a side per wave
+    constexpr int RG = TS / 32;                // 32-row DMA groups per plane
+    constexpr int NQ = 4 * RG;                 // DMA pieces per stage (4 planes)
+    constexpr int kTP = TS * kPK;                                   // bf16 per tile plane
+    __shared__ __attribute__((aligned(16))) __bf16 sm[2 * 4 * kTP];  // TS KiB: [buf][plane]
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
     const int wr = w >> 1, wc = w & 1;
-    // this lane's DMA sources: 16 per stage = plane q >> 2, rows 8 c .. 8 c + 7 (c = (q & 3) 4 + w)
-    // as 1 KiB pieces; lane -> row 8 c + lane / 8, LDS segment lane % 8 <- source segment
+    // this lane's DMA sources: NQ per stage = plane q / RG, rows 8 c .. 8 c + 7 (c = (q % RG) 4
+    // + w) as 1 KiB pieces; lane -> row 8 c + lane / 8, LDS segment lane % 8 <- source segment
     // (lane % 8) ^ ((row >> 1) & 7)
-    const __bf16* src[16];
+    const __bf16* src[16];   // NQ used (a dependent bound here drops the host-side kernel stub)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int pl = q >> 2, c = (q & 3) * 4 + w;
+    for (int q = 0; q < NQ; ++q) {
+        const int pl = q / RG, c = (q % RG) * 4 + w;
         const int row = 8 * c + (lane >> 3);
         const int seg = (lane & 7) ^ ((row >> 1) & 7);
-        int grow = (pl < 2 ? bi : bj) * 128 + row;
+        int grow = (pl < 2 ? bi : bj) * TS + row;
         grow = grow < n ? grow : n - 1;
         src[q] = ((pl & 1) ? Pl : Ph) + size_t(grow) * dp + 8 * seg;
     }
-    // DMAs of stage ks into buffer buf, pieces [q0, q0 + 4)
+    // DMAs of stage ks into buffer buf, pieces [q0, q0 + NQ / 4)
     auto issue4 = [&](int ks, int buf, int q0) {
 #pragma unroll
-        for (int q = q0; q < q0 + 4; ++q) {
-            const int pl = q >> 2, c = (q & 3) * 4 + w;
+        for (int q = q0; q < q0 + NQ / 4; ++q) {
+            const int pl = q / RG, c = (q % RG) * 4 + w;
             __bf16* dst = sm + (buf * 4 + pl) * kTP + c * 8 * kPK;
             __builtin_amdgcn_global_load_lds(src[q] + ks * kPK, (lds_void*)dst, 16, 0, 0);
         }
     };
-    f32x16 acc[2][2];
+    f32x16 acc[MA][MA];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < MA; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < MA; ++b)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
     auto frag = [&](int buf, int pl, int row, int kk) {
@@ -811,7 +820,7 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
     // fragment read, and every wave's reads of the buffer the next DMAs overwrite (stage ks-1's)
     // before those DMAs are issued.
 #pragma unroll
-    for (int q0 = 0; q0 < 16; q0 += 4) issue4(0, 0, q0);
+    for (int q0 = 0; q0 < NQ; q0 += NQ / 4) issue4(0, 0, q0);
     float dsc = 1.f;   // fp16 D2 scale (H), computed under the first stage's DMAs
     if constexpr (H) {
         __shared__ float red[4];
@@ -825,19 +834,19 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
         const bool more = ks + 1 < nks;
 #pragma unroll
         for (int kk = 0; kk < kPK / 16; ++kk) {
-            if (more) issue4(ks + 1, buf ^ 1, 4 * kk);
-            bf16x8 ah[2], al[2], bh[2], bl[2];
+            if (more) issue4(ks + 1, buf ^ 1, (NQ / 4) * kk);
+            bf16x8 ah[MA], al[MA], bh[MA], bl[MA];
 #pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                ah[m] = frag(buf, 0, wr * 64 + m * 32 + r, kk);
-                al[m] = frag(buf, 1, wr * 64 + m * 32 + r, kk);
-                bh[m] = frag(buf, 2, wc * 64 + m * 32 + r, kk);
-                bl[m] = frag(buf, 3, wc * 64 + m * 32 + r, kk);
+            for (int m = 0; m < MA; ++m) {
+                ah[m] = frag(buf, 0, wr * (TS / 2) + m * 32 + r, kk);
+                al[m] = frag(buf, 1, wr * (TS / 2) + m * 32 + r, kk);
+                bh[m] = frag(buf, 2, wc * (TS / 2) + m * 32 + r, kk);
+                bl[m] = frag(buf, 3, wc * (TS / 2) + m * 32 + r, kk);
             }
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < MA; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b) {
+                for (int b = 0; b < MA; ++b) {
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
@@ -847,16 +856,16 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
     __syncthreads();   // the last stage's reads are done before the diagonal epilogue reuses sm
     // epilogue: D2 = |a_i|^2 + |a_j|^2 - 2 <a_i, a_j>; C layout of 32x32: col = lane & 31,
     // row = (e & 3) + 8 (e >> 2) + 4 h
-    float nj[2];
+    float nj[MA];
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-        const int j = bj * 128 + wc * 64 + b * 32 + r;
+    for (int b = 0; b < MA; ++b) {
+        const int j = bj * TS + wc * (TS / 2) + b * 32 + r;
         nj[b] = nrm[j < n ? j : n - 1];
     }
     if (bi != bj) {
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
-            const int i0 = bi * 128 + wr * 64 + a * 32;
+        for (int a = 0; a < MA; ++a) {
+            const int i0 = bi * TS + wr * (TS / 2) + a * 32;
             float ni[16];
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
@@ -864,8 +873,8 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
                 ni[e] = nrm[i < n ? i : n - 1];
             }
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const int j = bj * 128 + wc * 64 + b * 32 + r;
+            for (int b = 0; b < MA; ++b) {
+                const int j = bj * TS + wc * (TS / 2) + b * 32 + r;
                 float dv[16];
 #pragma unroll
                 for (int e = 0; e < 16; ++e) dv[e] = ni[e] + nj[b] - 2.f * acc[a][b][e];
@@ -891,24 +900,25 @@ __global__ __launch_bounds__(256) void gram_pk_kernel(const __bf16* __restrict__
             }
         }
     } else {
-        // diagonal tile: stage [128][129] in LDS, store the upper triangle in both orientations
+        // diagonal tile: stage [TS][TS + 1] in LDS, store the upper triangle in both orientations
         float* tile = reinterpret_cast<float*>(sm);
+        constexpr int LT = TS + 1;
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < MA; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b)
+            for (int b = 0; b < MA; ++b)
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
-                    const int ti = wr * 64 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-                    const int tj = wc * 64 + b * 32 + r;
-                    const int i = bi * 128 + ti;
-                    tile[ti * 129 + tj] = nrm[i < n ? i : n - 1] + nj[b] - 2.f * acc[a][b][e];
+                    const int ti = wr * (TS / 2) + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    const int tj = wc * (TS / 2) + b * 32 + r;
+                    const int i = bi * TS + ti;
+                    tile[ti * LT + tj] = nrm[i < n ? i : n - 1] + nj[b] - 2.f * acc[a][b][e];
                 }
         __syncthreads();
-        for (int q = threadIdx.x; q < 128 * 128; q += 256) {
-            const int ti = q >> 7, tj = q & 127;
-            const int i = bi * 128 + ti, j = bi * 128 + tj;
-            if (i < n && j < n) dput<H>(D2, size_t(i) * ld + j, tj >= ti ? tile[ti * 129 + tj] : tile[tj * 129 + ti], dsc);
+        for (int q = threadIdx.x; q < TS * TS; q += 256) {
+            const int ti = q / TS, tj = q % TS;
+            const int i = bi * TS + ti, j = bi * TS + tj;
+            if (i < n && j < n) dput<H>(D2, size_t(i) * ld + j, tj >= ti ? tile[ti * LT + tj] : tile[tj * LT + ti], dsc);
         }
     }
 }
@@ -2539,13 +2549,20 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
         const int T2 = (L.n + 255) / 256;
         const bool t256 = gram_tile256(L, bt, T, T2);
         // one 256-tile per CU at a time: a last round short of a full one (stress: 528 tiles, 16
-        // in the third round, profiles/r04b_stress_kernel_stats.csv) runs as the 128-subtiles of
-        // those tiles instead (gram_pk_kernel's D2 is bitwise the 256-tile kernel's), when they
-        // fit one round (B = 64 NS: 128 tail tiles, two rounds of subtiles measured 224 -> 235 us)
+        // in the third round, profiles/r04b_stress_kernel_stats.csv) runs as subtiles of those
+        // tiles instead (gram_pk_kernel's D2 is bitwise the 256-tile kernel's), where they fit
+        // one round.  Round 6: 64-row subtiles (16 per tile, two workgroups per CU at 64 KiB of
+        // LDS) where they fit: stress 256 of them, one per CU, 18.8 us where 64 128-subtiles on a
+        // quarter of the chip took 31.4 (profiles/r06i_ab_gram_tail.txt); otherwise 128-subtiles
+        // (4 per tile).  More than one round of subtiles loses to a last round of 256-tiles: B =
+        // 64 NS, 128 tail tiles, 2,048 64-subtiles 58 us against ~35 for the round, and two rounds
+        // of 128-subtiles 224 -> 235 us (round 5).  GLL_KNOB_GRAM_TAIL: 1 no tail, 2 128-subtiles.
         const int64_t nt2 = int64_t(bt.B) * T2 * (T2 + 1) / 2;
         const int cus = device_cus();
+        const int tk = knob(GLL_KNOB_GRAM_TAIL);
         int64_t tail = t256 && nt2 > cus ? nt2 % cus : 0;
-        if (tail * 4 > cus || knob(GLL_KNOB_GRAM_TAIL) == 1) tail = 0;
+        const int sub = (tk != 2 && tail * 16 <= 2 * int64_t(cus)) ? 16 : 4;   // subtiles per tile
+        if ((sub == 4 && tail * 4 > cus) || tk == 1) tail = 0;
         // (Measured and dropped: the subtiles split further over 4 k-slices summed by a reduce
         // kernel, 256 workgroups instead of 64: 250 -> 260 us, profiles/r04u_ab_tail.txt.)
         prof_begin(GLL_K_GRAM, s);
@@ -2560,12 +2577,16 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
             launch_k(H ? gram_pk2_kernel<true> : gram_pk2_kernel<false>,
                      dim3(unsigned(nt2 - tail)), 512, 0, s, Ph, Pl, nrm, L.n, L.dp, T2, D2,
                      L.ldD, bt.ws, d2s);
-            if (tail > 0)
-                launch_k(H ? gram_pk_kernel<true> : gram_pk_kernel<false>,
+            if (tail > 0 && sub == 4)
+                launch_k(H ? gram_pk_kernel<true, 128> : gram_pk_kernel<false, 128>,
                          dim3(unsigned(4 * tail)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T, D2, L.ldD,
                          bt.ws, d2s, int(nt2 - tail));
+            else if (tail > 0)
+                launch_k(H ? gram_pk_kernel<true, 64> : gram_pk_kernel<false, 64>,
+                         dim3(unsigned(16 * tail)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp,
+                         (L.n + 63) / 64, D2, L.ldD, bt.ws, d2s, int(nt2 - tail));
         } else {
-            launch_k(H ? gram_pk_kernel<true> : gram_pk_kernel<false>,
+            launch_k(H ? gram_pk_kernel<true, 128> : gram_pk_kernel<false, 128>,
                      dim3(unsigned(bt.B * T * (T + 1) / 2)), 256, 0, s, Ph, Pl, nrm, L.n, L.dp, T,
                      D2, L.ldD, bt.ws, d2s, -1);
         }

@@ -93,7 +93,8 @@ extern "C" {
 #define GLL_KNOB_GRID_CAP 1   /* whole-GPU CG: co-resident workgroup capacity */
 #define GLL_KNOB_GRAM_TILE 2  /* pre-split Gram: 128- or 256-row tiles */
 #define GLL_KNOB_SEL_FORM 3   /* kNN select form: 1 latency (PG 2), 2 occupancy (knn.hip) */
-#define GLL_KNOB_GRAM_TAIL 4  /* 1: no 128-subtile tail after the 256-tile Gram (knn.hip) */
+#define GLL_KNOB_GRAM_TAIL 4  /* 256-tile Gram's short last round: 1 none, 2 as 128-subtiles
+                               * instead of 64-subtiles (knn.hip) */
 #define GLL_KNOB_ROW_PRE 5    /* row build label prefetch: 1 on, 2 off (rows.hip) */
 #define GLL_KNOB_COUNT 6
 int gll_set_knob(int knob, int value);

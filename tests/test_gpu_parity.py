@@ -1360,13 +1360,13 @@ def test_fused_backward_handoff_with_uneven_column_solves(live):
 
 @pytest.mark.parametrize("cfg,B,n_extra,d", [("ns", 3, 0, None), ("fullysup", 2, 0, None),
                                              ("ns", 2, 37, 100), ("ns", 26, 0, None),
-                                             ("ns", 26, 37, 100)])
+                                             ("ns", 26, 37, 100), ("ns", 64, 0, None)])
 def test_gram_256_tiles_match_128_tiles(cfg, B, n_extra, d, monkeypatch):
     """The 256-tile pre-split Gram (knn.hip gram_pk2_kernel, 8 waves) against the 128-tile one
     (gram_pk_kernel) on batches, ragged n and d included: the same k order and epilogue, so U
     and grad_X agree bitwise (the GLL_KNOB_GRAM_TILE test knob forces either).  B = 26 (n 1,000
-    and 1,037): 260 256-tiles on a 256-CU device, whose short last round runs as 128-subtiles (the
-    launch's tail)."""
+    and 1,037): 260 256-tiles on a 256-CU device, whose short last round runs as 64-subtiles (the
+    launch's tail); B = 64: 640 256-tiles, a third round of 256-tiles."""
     from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth
     GLL = _gll()
     c = dict(CONFIGS[cfg])
@@ -1396,17 +1396,18 @@ def test_gram_256_tiles_match_128_tiles(cfg, B, n_extra, d, monkeypatch):
 
 
 def test_gram_tail_changes_no_result():
-    """The stress Gram (8,192 x 1024: 528 256-tiles on 256 CUs) runs its 16-tile last round as 64
-    128-subtiles (gram_pk_kernel, bitwise the 256-tile kernel's D2); GLL_KNOB_GRAM_TAIL = 1 runs a
-    third 256-tile round instead.  The kNN lists, distances and eps are bitwise the same, and no
-    row needs the exact rescan (GLL.py:183,205)."""
+    """The stress Gram (8,192 x 1024: 528 256-tiles on 256 CUs) runs its 16-tile last round as 256
+    64-subtiles (gram_pk_kernel<H, 64>, round 6; bitwise the 256-tile kernel's D2);
+    GLL_KNOB_GRAM_TAIL = 2 runs it as 64 128-subtiles (round 5), 1 as a third 256-tile round.  The
+    kNN lists, distances and eps are bitwise the same, and no row needs the exact rescan
+    (GLL.py:183,205)."""
     from graphlearninglayer_amd import _lib
     from graphlearninglayer_amd.synth import CONFIGS, synth
     c = CONFIGS["stress"]
     X, _ = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=5)
     outs = []
     try:
-        for tail in (0, 1):
+        for tail in (0, 1, 2):
             _lib.set_knob(_lib.KNOB_GRAM_TAIL, tail)
             g = _gpu_knn(X, c["k"], "auto")
             outs.append({key: g[key].cpu().numpy() for key in ("knn_idx", "knn_d2", "eps")})
@@ -1415,6 +1416,7 @@ def test_gram_tail_changes_no_result():
         _lib.set_knob(_lib.KNOB_GRAM_TAIL, 0)
     for key in outs[0]:
         np.testing.assert_array_equal(outs[1][key], outs[0][key])
+        np.testing.assert_array_equal(outs[2][key], outs[0][key])
 
 
 @pytest.mark.parametrize("eps", [1.0, "auto"])
