@@ -1044,7 +1044,77 @@ __global__ __launch_bounds__(NT) void cg_grad_fused_kernel(EllCgArgs c, EdgeArgs
     constexpr int EB = ND <= 2 ? 16 : 8;   // grad_spmm_kernel's single-graph (WIDE) batch
     __shared__ int s_ok;
     const int lane = lane_id();
-    const int i0 = (int(blockIdx.x) - C) * (NT / kWave) + (threadIdx.x >> 6);
+    // XCD-local rows (round 6).  A row's gradient gathers its neighbours' X rows, and ~86% of
+    // kNN edges join rows of one class, so the rows are taken in class order --
+    // argmax of P = [Y; U], the forward's output -- and each XCD's workgroups (block b runs on
+    // XCD b % 8: dispatch order, §3.5, a speed assumption only) take a contiguous run of that
+    // order: an XCD then gathers mostly the X rows of one or two classes, which its L2 holds,
+    // instead of every XCD refilling all of X (16 MB of counter bytes for a 2 MB X at NS,
+    // profiles/r05zzzz_pmc_ns.json).  Each gradient workgroup sorts the rows itself (a stable
+    // counting sort in its LDS) while the adjoint solves run; a row's result does not depend on
+    // which wave computes it, so the gradient is bitwise that of the row-index order.
+    int i0;
+    {
+        extern __shared__ __attribute__((aligned(16))) float smem[];
+        int* srt = reinterpret_cast<int*>(smem);   // [n] rows in class order
+        int* crk = srt + a.n;                      // [n] class << 16 | rank in its 64-row chunk
+        const int nch = (a.n + kWave - 1) / kWave;
+        int* cnt = crk + a.n;                      // [nch][NC] rows per (chunk, class)
+        constexpr int NW = NT / kWave;
+        const int w = threadIdx.x >> 6;
+        for (int q = w; q < nch; q += NW) {   // wave-uniform
+            const int i = q * kWave + lane;
+            int cls = -1;
+            if (i < a.n) {
+                float bv = -3.0e38f;
+                cls = 0;
+#pragma unroll
+                for (int k = 0; k < NC; k += 2) {
+                    const f32x2 v = *reinterpret_cast<const f32x2*>(a.P + size_t(i) * NC + k);
+                    if (v.x > bv) bv = v.x, cls = k;
+                    if (v.y > bv) bv = v.y, cls = k + 1;
+                }
+            }
+            int rnk = 0;
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                const uint64_t mk = __ballot(cls == k);
+                if (cls == k) rnk = lanes_below(mk);
+                if (lane == k) cnt[q * NC + k] = __popcll(mk);
+            }
+            if (i < a.n) crk[i] = (cls << 16) | rnk;
+        }
+        __syncthreads();
+        if (threadIdx.x < NC) {   // each (chunk, class) run's first position, class-major
+            const int k = threadIdx.x;
+            int before = 0;
+            for (int kk = 0; kk < k; ++kk)
+                for (int q = 0; q < nch; ++q) before += cnt[q * NC + kk];
+            for (int q = 0; q < nch; ++q) {
+                const int c0 = cnt[q * NC + k];
+                cnt[q * NC + k] = before;
+                before += c0;
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < a.n; i += NT) {
+            const int v = crk[i];
+            srt[cnt[(i / kWave) * NC + (v >> 16)] + (v & 0xffff)] = i;
+        }
+        __syncthreads();
+        // this workgroup's rank in XCD-major order of the gradient workgroups
+        const int G = int(gridDim.x) - C, b = int(blockIdx.x), x = b & 7;
+        int ord = 0;
+#pragma unroll
+        for (int xx = 0; xx < 8; ++xx) {
+            const int f = C + ((xx - C % 8 + 8) & 7);   // first gradient block on XCD xx
+            const int cx = f < C + G ? (C + G - 1 - f) / 8 + 1 : 0;
+            if (xx < x) ord += cx;
+        }
+        ord += (b - (C + ((x - C % 8 + 8) & 7))) >> 3;
+        const int pos = ord * NW + w;
+        i0 = pos < a.n ? srt[pos] : a.n;
+    }
     const bool live = i0 < a.n;
     const int i = live ? i0 : 0;
     const int d = a.d;
@@ -1248,6 +1318,10 @@ static hipError_t run_fused(const Layout& L, void* ws, const TB* b, const float*
     if (cap > eu_bound) cap = eu_bound;
     if (cap < 0) cap = 0;
     lds += size_t(cap) * 8;
+    // the gradient workgroups' counting sort of the rows (class order): 2 n ints + the chunk table
+    const size_t sort_lds = size_t(L.n) * 8 + size_t((L.n + kWave - 1) / kWave) * 10 * 4;
+    if (sort_lds > kLdsDyn) return hipErrorNotSupported;
+    if (lds < sort_lds) lds = sort_lds;
     auto fn = cg_grad_fused_kernel<NT, S, TB, ND>;
     allow_full_lds(reinterpret_cast<const void*>(fn));
     const int G = L.C + (L.n + NT / kWave - 1) / (NT / kWave);
