@@ -1306,15 +1306,17 @@ def _fwd_bwds_c_abi(X, Y, k, tau, eps, gbar, flags=0, backward_calls=1):
     return U.cpu().numpy(), grads, st
 
 
-@pytest.mark.parametrize("cfg", ["plumbing", "ns"])
+@pytest.mark.parametrize("cfg", ["plumbing", "ns", "wide_base"])
 def test_fused_backward_equals_two_launches_bitwise(cfg):
     """The fused backward (adjoint CG + feature gradient in one launch, solve.hip
     cg_grad_fused_kernel: single small graphs, fixed eps) against the same two kernels as two
     launches (GLL_FLAG_BWD_UNFUSED): bitwise equal, and equal again on a second backward over
-    the same workspace (the hand-off counters re-arm); against the float64 oracle at 1e-4."""
+    the same workspace (the hand-off counters re-arm); against the float64 oracle at 1e-4.
+    The gradient waves take the rows in class order (round 6); `wide_base`
+    (3,500 labeled + 500 unlabeled rows at d = 128) sorts 63 64-row chunks."""
     from graphlearninglayer_amd import _lib
     from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth
-    c = CONFIGS[cfg]
+    c = CONFIGS[cfg] if cfg in CONFIGS else dict(base=3500, batch=500, d=128, k=10, r=1.0)
     X, lab = synth(c["base"], c["batch"], c["d"], r=c["r"], seed=6)
     Y = one_hot(lab[: c["base"]])
     g = seeded_gbar(c["batch"], 10, 17)
