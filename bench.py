@@ -312,8 +312,16 @@ def batched_measure(c, eps, tau, k, B, gstats, dev, rank, steps=20, warmup=5):
         step()
     torch.cuda.synchronize()
     kid = [_lib.kernel_name(q) for q in range(_lib.K_COUNT)].index("cg_kernel")
-    # every launch of every kernel bracketed (a lone bracket on the CG reads long: see main()); an
-    # untimed pass first fills the event pool, so the timed one creates no event
+    # the batch throughput: a pass with no kernel events (they cost the step time, main())
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    # the CG launch times: every launch of every kernel bracketed (a lone bracket on the CG reads
+    # long: see main()) in a second pass; an untimed pass first fills the event pool, so the
+    # measured one creates no event
     for q in range(_lib.K_COUNT):
         _lib.prof_enable(q, 1)
     for _ in range(steps):
@@ -322,11 +330,11 @@ def batched_measure(c, eps, tau, k, B, gstats, dev, rank, steps=20, warmup=5):
     for q in range(_lib.K_COUNT):
         _lib.prof_read(q)
         _lib.prof_enable(q, 1)
-    t0 = time.perf_counter()
+    t1 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed_ev = time.perf_counter() - t1
     ms, cnt = _lib.prof_read(kid)
     for q in range(_lib.K_COUNT):
         _lib.prof_enable(q, 0)
@@ -352,8 +360,10 @@ def batched_measure(c, eps, tau, k, B, gstats, dev, rank, steps=20, warmup=5):
     roof.update(cg_roofline_extras(B * work, B * cg_iter_work, avg_s, traffic))
     return {"B": B, "value": round(B * steps / elapsed, 3), "unit": "calls/s",
             "ms_per_step": round(1e3 * elapsed / steps, 4),
-            "note": "one fwd+bwd of the batched entry point = B graphs; every CG launch "
-                    "timed by events carried in its dispatch packet",
+            "events_pass_ms_per_step": round(1e3 * elapsed_ev / steps, 4),
+            "note": "one fwd+bwd of the batched entry point = B graphs, timed with no kernel "
+                    "events; every CG launch timed by events carried in its dispatch packet in "
+                    "a second pass (events_pass_ms_per_step)",
             "roofline": roof, "cg_iters_fwd_bwd": [it_f, it_b],
             "gram_mfma_pmc": gram_mfma_pmc(f"{c['name']}_b{B}")}
 
