@@ -177,9 +177,10 @@ def cg_roofline_extras(work_spmv, work_iter, avg_s, traffic):
 # C-ABI kernel ids (gll_kernel_name) -> device symbols as rocprofv3 names them.  The Gram id
 # covers several launches on the pre-split route: gram_split_kernel (hi/lo planes),
 # gram_pk2_kernel (the main 256-tile GEMM) and gram_pk_kernel (its 128-subtile tail); single
-# small graphs run gram_bf3s_kernel alone.  The main kernel is listed first.
+# small graphs run gram_bf3s_kernel (256 < d <= 512) or gram_bf3h_kernel (d <= 128) alone.
+# The main kernel is listed first.
 PMC_SYMBOLS = {"gram_d2_kernel": ["gram_pk2_kernel", "gram_bf3s_kernel", "gram_bf3w_kernel",
-                                  "gram_bf3_kernel", "gram_pk_kernel"],
+                                  "gram_bf3_kernel", "gram_bf3h_kernel", "gram_pk_kernel"],
                "knn_select_kernel": ["knn_select_kernel", "knn_select_wide_kernel"],
                "row_build_kernel": ["row_build_kernel"],
                "cg_kernel": ["cg_ell_kernel", "cg_vr_kernel", "cg_gv_kernel", "cg_grid_kernel",
@@ -189,7 +190,7 @@ PMC_SYMBOLS = {"gram_d2_kernel": ["gram_pk2_kernel", "gram_bf3s_kernel", "gram_b
 # the Gram's launches by role, for the MFMA counters (reported separately)
 GRAM_ROLES = (("main", "gram_pk2_kernel"), ("tail", "gram_pk_kernel"),
               ("single", "gram_bf3s_kernel"), ("inline", "gram_bf3w_kernel"),
-              ("inline", "gram_bf3_kernel"))
+              ("inline", "gram_bf3_kernel"), ("inline", "gram_bf3h_kernel"))
 
 
 def build_profile_tags():

@@ -104,21 +104,42 @@ constexpr int kBS = kBP + 8;        // LDS plane row stride (bf16)
 // and streaming it out leaves less for the end-of-kernel L2 write-back (NS call 71.4 -> 70.5 us
 // over 300 calls, alternating builds, tools/ab_flags.py --lib; on the 128-tile kernel the same
 // change measured +0.6% at stress and -1.3% at B = 64, so that one keeps ordinary stores).
-template <typename NF>
+// NT = 512 is the half tile (gram_bf3h_kernel): 2 feature halves instead of 4 quarters, and
+// 8 tile elements per thread; slot s of wave w holds rows 16 s + 2 w (lanes 0..31) and
+// 16 s + 2 w + 1 (lanes 32..63), reduced per half wave.
+template <int NT = 1024, typename NF>
 __device__ __forceinline__ void bf3_epilogue(const f32x16& acc, const float (&sq)[8], float* smem,
                                              float (*sqp)[16], float* nrm, NF nrm_of, int bi,
                                              int bj, int n, float* __restrict__ D2, int ld,
                                              float* __restrict__ Dz) {
+    static_assert(NT == 1024 || NT == 512, "bf3_epilogue: 1024- or 512-thread tiles");
+    constexpr int KQ = NT / 256;     // feature groups per quadrant
+    constexpr int EP = 4096 / NT;    // tile elements per thread
+    constexpr int CPR = 64 / EP;     // threads per tile row
     const int tid = threadIdx.x;
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
     const int qd = w & 3, kq = w >> 2;
-    // row norms: slot s of wave w is tile row 16 s + w, its features spread over the wave
+    if constexpr (NT == 1024) {
+        // row norms: slot s of wave w is tile row 16 s + w, its features spread over the wave
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-        const float t = wave_sum_dpp(sq[s]);
-        if (lane == 0) sqp[s][w] = t;
+        for (int s = 0; s < 8; ++s) {
+            const float t = wave_sum_dpp(sq[s]);
+            if (lane == 0) sqp[s][w] = t;
+        }
+    } else {
+        // half-wave sums: row sums of 16 lanes, then row_bcast15 carries row 0 into row 1 and
+        // row 2 into row 3 (lane 31: lanes 0..31, lane 63: lanes 32..63)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            float t = dpp_add<0xB1, 0xf>(sq[s]);
+            t = dpp_add<0x4E, 0xf>(t);
+            t = dpp_add<0x141, 0xf>(t);
+            t = dpp_add<0x140, 0xf>(t);
+            t = dpp_add<0x142, 0xa>(t);
+            if ((lane & 31) == 31) sqp[s][2 * w + h] = t;
+        }
     }
     __syncthreads();   // fragment reads done: the planes become partial / tile space
     // partial quadrant -> LDS part[kq][qd][32][33] (C layout: col = lane & 31,
@@ -128,62 +149,70 @@ __device__ __forceinline__ void bf3_epilogue(const f32x16& acc, const float (&sq
     for (int e = 0; e < 16; ++e) pw[((e & 3) + 8 * (e >> 2) + 4 * h) * 33 + r] = acc[e];
     if (tid < 128) nrm[tid] = nrm_of(tid);
     __syncthreads();
-    // tile element (ti, tj..tj+3): sum of the 4 feature quarters, fixed order
-    const int ti = tid >> 4, tj = 4 * (tid & 15);
-    float v[4];
+    // tile element (ti, tj..tj+EP-1): sum of the KQ feature groups, fixed order
+    const int ti = tid / CPR, tj = EP * (tid % CPR);
+    float v[EP];
     {
         const int q = 2 * (ti >> 5) + (tj >> 5), rr = ti & 31;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < EP; ++e) {
             const int cc = (tj & 31) + e;
             float t = 0.f;
 #pragma unroll
-            for (int k4 = 0; k4 < 4; ++k4) t += smem[(k4 * 4 + q) * 32 * 33 + rr * 33 + cc];
+            for (int k4 = 0; k4 < KQ; ++k4) t += smem[(k4 * 4 + q) * 32 * 33 + rr * 33 + cc];
             v[e] = t;
         }
     }
     __syncthreads();
-    float* tile = smem + 16 * 32 * 33;   // [64][65], past the partials
+    float* tile = smem + KQ * 4 * 32 * 33;   // [64][65], past the partials
 #pragma unroll
-    for (int e = 0; e < 4; ++e) tile[ti * 65 + tj + e] = nrm[ti] + nrm[64 + tj + e] - 2.f * v[e];
+    for (int e = 0; e < EP; ++e) tile[ti * 65 + tj + e] = nrm[ti] + nrm[64 + tj + e] - 2.f * v[e];
     __syncthreads();
-    // direct orientation: row bi*64 + ti, columns bj*64 + tj .. +3; a diagonal tile takes the
-    // upper triangle for both halves so D2 stays bitwise symmetric
+    // direct orientation: row bi*64 + ti, columns bj*64 + tj .. +EP-1; a diagonal tile takes
+    // the upper triangle for both halves so D2 stays bitwise symmetric
     const int i = bi * 64 + ti;
     if (i < n) {
-        float o[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int jj = tj + e;
-            o[e] = (bi == bj && jj < ti) ? tile[jj * 65 + ti] : tile[ti * 65 + jj];
-        }
-        float* dst = D2 + size_t(i) * ld + bj * 64 + tj;
-        float* dz = Dz ? Dz + size_t(i) * ld + bj * 64 + tj : nullptr;
-        if (bj * 64 + tj + 4 <= n) {
-            __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<f32x4*>(dst));
-            if (dz) __builtin_nontemporal_store(f32x4{0.f, 0.f, 0.f, 0.f}, reinterpret_cast<f32x4*>(dz));
-        } else {
+        for (int c = 0; c < EP; c += 4) {
+            float o[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (bj * 64 + tj + e < n) {
-                    dst[e] = o[e];
-                    if (dz) dz[e] = 0.f;
-                }
+            for (int e = 0; e < 4; ++e) {
+                const int jj = tj + c + e;
+                o[e] = (bi == bj && jj < ti) ? tile[jj * 65 + ti] : tile[ti * 65 + jj];
+            }
+            const int j0 = bj * 64 + tj + c;
+            float* dst = D2 + size_t(i) * ld + j0;
+            float* dz = Dz ? Dz + size_t(i) * ld + j0 : nullptr;
+            if (j0 + 4 <= n) {
+                __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<f32x4*>(dst));
+                if (dz) __builtin_nontemporal_store(f32x4{0.f, 0.f, 0.f, 0.f}, reinterpret_cast<f32x4*>(dz));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (j0 + e < n) {
+                        dst[e] = o[e];
+                        if (dz) dz[e] = 0.f;
+                    }
+            }
         }
     }
-    // mirrored orientation: row bj*64 + ti, columns bi*64 + tj .. +3 from the tile's column ti
+    // mirrored orientation: row bj*64 + ti, columns bi*64 + tj .. from the tile's column ti
     const int jr = bj * 64 + ti;
     if (bi != bj && jr < n) {
-        float o[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = tile[(tj + e) * 65 + ti];
-        float* dst = D2 + size_t(jr) * ld + bi * 64 + tj;
-        if (bi * 64 + tj + 4 <= n) {
-            __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<f32x4*>(dst));
-        } else {
+        for (int c = 0; c < EP; c += 4) {
+            float o[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (bi * 64 + tj + e < n) dst[e] = o[e];
+            for (int e = 0; e < 4; ++e) o[e] = tile[(tj + c + e) * 65 + ti];
+            const int j0 = bi * 64 + tj + c;
+            float* dst = D2 + size_t(jr) * ld + j0;
+            if (j0 + 4 <= n) {
+                __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<f32x4*>(dst));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (j0 + e < n) dst[e] = o[e];
+            }
         }
     }
 }
@@ -302,6 +331,94 @@ __global__ __launch_bounds__(1024) void gram_bf3_kernel(const float* __restrict_
     bf3_epilogue(acc, sq, smem, sqp, nrm, [&](int t) { return sqp[t >> 4][t & 15]; }, bi, bj, n,
                  D2, ld, nullptr);
     GLL_TRACE_PT(14);
+}
+
+// K1a'' (d <= 128, fewer than 512 64-tiles): the same tile at half the workgroup.  The
+// 1024-thread tile stages kBP = 256 features per phase, so at d <= 128 half its loads and half
+// its MFMAs run on zero features, and its 151 KiB of LDS holds one workgroup per CU: FullySup's
+// 300 tiles (n = 1500) ran as two rounds over 256 CUs.  Here 8 waves (4 quadrants x 2 feature
+// halves) stage 128 rows x 128 features in 70 KiB: two workgroups per CU, one round.  Lanes
+// 0..31 and 32..63 of a wave hold two rows (512 contiguous bytes each), so the loads stay
+// coalesced; the epilogue is bf3_epilogue<512>.
+constexpr int kHP = 128;          // features of the half tile
+constexpr int kHS = kHP + 8;      // its LDS plane row stride (bf16)
+template <bool VEC>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+void gram_bf3h_kernel(const float* __restrict__ X, int n, int d, int T, float* __restrict__ D2,
+                      int ld, int32_t* __restrict__ status, int32_t* __restrict__ rev_cnt,
+                      size_t xs, size_t wss) {
+    X = gshift_br(X, xs);
+    D2 = gshift_br(D2, wss);
+    status = gshift_br(status, wss);
+    rev_cnt = gshift_br(rev_cnt, wss);
+    constexpr int kPlane = 128 * kHS;
+    static_assert(2 * kPlane * 2 >= (8 * 32 * 33 + 64 * 65) * 4, "half tile: epilogue space");
+    __shared__ __attribute__((aligned(16))) __bf16 smem_h[2 * kPlane];
+    __shared__ float sqp[8][16];
+    __shared__ float nrm[128];
+    float* smem = reinterpret_cast<float*>(smem_h);
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    int bi = 0, rem = xcd_tile(bx(), gridDim.x);
+    while (rem >= T - bi) {
+        rem -= T - bi;
+        ++bi;
+    }
+    const int bj = bi + rem;
+    {   // per-call reset of the counters the select kernel accumulates into
+        const int g = bx() * 512 + tid;
+        if (g < kStWords) status[g] = 0;
+        for (int q = g; q < n; q += gridDim.x * 512) rev_cnt[q] = 0;
+    }
+    const int fo = 4 * r;   // this lane's 4 features
+    // slot s -> LDS row 16 s + 2 w + h (0..63 rows bi, 64..127 rows bj; rows past n clamped);
+    // the centre row's load is issued first
+    const f32x4 c = load4_raw<VEC>(X, fo, d);
+    f32x4 v[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const int R = 16 * s + 2 * w + h;
+        const int row = R < 64 ? bi * 64 + R : bj * 64 + R - 64;
+        v[s] = load4_raw<VEC>(X + size_t(row < n ? row : n - 1) * d, fo, d);
+    }
+    float sq[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const f32x4 f = mask4<VEC>(v[s] - c, fo, d);
+        sq[s] = f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+        bf16x4 hv, lv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const __bf16 hb = static_cast<__bf16>(f[e]);
+            hv[e] = hb;
+            lv[e] = static_cast<__bf16>(f[e] - static_cast<float>(hb));
+        }
+        const int o = (16 * s + 2 * w + h) * kHS + fo;
+        *reinterpret_cast<bf16x4*>(smem_h + o) = hv;
+        *reinterpret_cast<bf16x4*>(smem_h + kPlane + o) = lv;
+    }
+    __syncthreads();
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    const int qd = w & 3, kq = w >> 2;   // quadrant, feature half
+    const int qa = qd >> 1, qb = qd & 1;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+        const int kk = 64 * kq + 16 * st + 8 * h;
+        const int oa = (32 * qa + r) * kHS + kk, ob = (64 + 32 * qb + r) * kHS + kk;
+        const bf16x8 ha = *reinterpret_cast<const bf16x8*>(smem_h + oa);
+        const bf16x8 la = *reinterpret_cast<const bf16x8*>(smem_h + kPlane + oa);
+        const bf16x8 hb = *reinterpret_cast<const bf16x8*>(smem_h + ob);
+        const bf16x8 lb = *reinterpret_cast<const bf16x8*>(smem_h + kPlane + ob);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(la, hb, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha, lb, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha, hb, acc, 0, 0, 0);
+    }
+    bf3_epilogue<512>(acc, sq, smem, sqp, nrm, [&](int t) { return sqp[t >> 4][t & 15]; }, bi, bj,
+                      n, D2, ld, nullptr);
 }
 
 // K1a' (one graph, n <= 1024, 256 < d <= 512): the same tile over HALF the features.  With
@@ -2606,6 +2723,14 @@ hipError_t launch_gram(const Layout& L, const Batch& bt, void* ws, const float* 
     const int T64 = (L.n + 63) / 64;
     const dim3 grid(T64 * (T64 + 1) / 2, bt.B);
     prof_begin(GLL_K_GRAM, s);
+    if (L.d <= kHP) {   // 1024-thread tile 17.4 -> 9.5 us at FullySup (profiles/r06v_ab_*.txt)
+        if (vec)
+            launch_k(gram_bf3h_kernel<true>, grid, 512, 0, s, X, L.n, L.d, T64, D2, L.ldD, st, rc, bt.x, bt.ws);
+        else
+            launch_k(gram_bf3h_kernel<false>, grid, 512, 0, s, X, L.n, L.d, T64, D2, L.ldD, st, rc, bt.x, bt.ws);
+        prof_end(GLL_K_GRAM, s);
+        return launch_status("knn.hip:launch_gram(bf3h)");
+    }
     if (vec)
         launch_k(gram_bf3_kernel<true>, grid, 1024, 0, s, X, L.n, L.d, T64, D2, L.ldD, st, rc, bt.x, bt.ws);
     else
