@@ -177,16 +177,17 @@ def test_split_phase_gram_shapes(n, d, eps):
 
 
 @pytest.mark.parametrize("n,d,eps", [(1500, 128, 1.0), (777, 37, "auto"), (1984, 125, 1.0),
-                                     (130, 128, "auto"), (300, 1, 1.0)])
+                                     (130, 128, "auto"), (300, 2, 1.0)])
 def test_half_tile_gram_shapes(n, d, eps):
     """Single graphs with d <= 128 and fewer than 512 64-tiles take the 512-thread half tile
     (knn.hip gram_bf3h_kernel): FullySup's shape, a scalar-load ragged shape (777 x 37), the
     largest triangle on this route (31 tiles a side: 496), d = 125 (lanes past d in the last
-    feature group), two tiles of which one nearly empty (130) and d = 1.  Exact kNN sets
-    against float64 and U / grad_X against the oracle."""
+    feature group), two tiles of which one nearly empty (130) and d = 2 (unit rows on a circle;
+    at d = 1 every row is +-1, all ties).  Exact kNN sets against float64 and U / grad_X
+    against the oracle."""
     from graphlearninglayer_amd.synth import one_hot, seeded_gbar, synth
     base = n // 5
-    X, lab = synth(base, n - base, d, r=1.0, seed=13)
+    X, lab = synth(base, n - base, d, r=1.0, latent=min(16, d), seed=13)
     Y = one_hot(lab[:base])
     g = seeded_gbar(n - base, 10, 5)
     U, grad = _run(X, Y, 0.07, eps, 10, g)
