@@ -134,7 +134,22 @@ __device__ __forceinline__ void block_sum3_read(const float* q, float& a, float&
         constexpr int NW = NT / kWave;
         constexpr int NQ = NW < 4 ? 4 : NW;
         a = b = c = 0.f;
-        if constexpr (NW % 4 == 0) {
+        if constexpr (NW == 2 || NW == 4 || NW == 8 || NW == 16) {
+            // one ds_read_b32 per lane (lane l < 3 NW: partial l % NW of value l / NW) and DPP
+            // sums over aligned groups of NW lanes, instead of 3 NW / 4 ds_read_b128 that every
+            // lane of every wave repeats (8 LDS cycles each, all waves right after the barrier)
+            const int lane = lane_id();
+            const int idx = (lane / NW) * NQ + lane % NW;
+            const float t = q[lane < 3 * NW ? idx : 0];
+            float v = lane < 3 * NW ? t : 0.f;
+            v = dpp_add<0xB1, 0xf>(v);                              // pairs
+            if constexpr (NW >= 4) v = dpp_add<0x4E, 0xf>(v);       // quads
+            if constexpr (NW >= 8) v = dpp_add<0x141, 0xf>(v);      // half rows
+            if constexpr (NW >= 16) v = dpp_add<0x140, 0xf>(v);     // rows
+            a = readlane_f(v, 0);
+            b = readlane_f(v, NW);
+            c = readlane_f(v, 2 * NW);
+        } else if constexpr (NW % 4 == 0) {
 #pragma unroll
             for (int w = 0; w < NW; w += 4) {
                 const f32x4 va = *reinterpret_cast<const f32x4*>(q + w);

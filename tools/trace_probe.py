@@ -19,7 +19,7 @@ from graphlearninglayer_amd.synth import CONFIGS, one_hot, seeded_gbar, synth  #
 
 TICK_US = 0.01
 # _obj/ stays on this side (.gpurunignore): copy the trace build next to this script to ship it
-_tl = os.path.join(ROOT, "tools", "libgll_trace.so")
+_tl = os.environ.get("TRACE_LIB", os.path.join(ROOT, "tools", "libgll_trace.so"))
 lib = ct.CDLL(_tl if os.path.exists(_tl) else
               os.path.join(ROOT, "graphlearninglayer_amd", "_obj", "libgll_trace.so"))
 lib.gll_workspace_bytes.restype = ct.c_size_t
